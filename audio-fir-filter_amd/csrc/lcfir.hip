@@ -1,0 +1,483 @@
+// lcfir.hip -- C ABI (include/lcfir.h) over the gfx950 FIR kernels.
+//
+// Host-side responsibilities:
+//   * one lcfir_ctx per (device, filter): the taps live in HBM for the life
+//     of the context (the reference builds its WindowedSinc once per file,
+//     ProcessFile.cp:47-50);
+//   * lcfir_apply_range: the reference's apply_filter_range call
+//     (FilterCore.h:20-27) on host buffers, re-entrant for the concurrent
+//     disjoint-range calls of ProcessFile.cp:71-78.  Each call borrows a
+//     staging slot (stream + device buffers) from a per-device pool, copies
+//     x[start-half, end+half) in, runs the kernel, copies y[start,end) out;
+//   * device-pointer entry points that never synchronise the host.
+// No CPU fallback exists: if the device or the kernels are unusable every
+// call fails with LCFIR_EDEVICE and a message.
+#include "lcfir.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "fir_direct.hpp"
+#include "fir_fft.hpp"
+#include "peak_scale.hpp"
+
+struct lcfir_ctx {
+    int device = 0;
+    int32_t ntaps = 0;
+    int32_t half = 0;
+    int method = LCFIR_METHOD_AUTO;
+    double *d_taps = nullptr;
+    lcfir::FftPlan fft; // frequency-domain filter, built lazily
+    std::mutex fft_mu;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define LCFIR_HIP(expr)                                                                          \
+    do {                                                                                         \
+        hipError_t e_ = (expr);                                                                  \
+        if (e_ != hipSuccess)                                                                    \
+            return fail(LCFIR_EDEVICE, "%s failed: %s", #expr, hipGetErrorString(e_));           \
+    } while (0)
+
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = false;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        ok = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+// ---- direct kernel configuration ---------------------------------------
+constexpr int kDirR = 16;   // outputs per lane
+constexpr int kDirNT = 256; // threads per workgroup (4 waves)
+constexpr int kDirTC = 256; // taps per LDS stage -> 39 KB LDS -> 4 workgroups / CU
+
+int launch_direct(lcfir::DirectParams p, int nch, hipStream_t s) {
+    const int64_t count = p.end - p.start;
+    if (count <= 0 || nch <= 0) return LCFIR_OK;
+    constexpr int BO = kDirR * kDirNT;
+    p.tc = kDirTC;
+    const int64_t gx = (count + BO - 1) / BO;
+    if (gx > 0x7fffffff || nch > 65535) return fail(LCFIR_EINVAL, "range too large for one launch");
+    const size_t lds = lcfir::direct_lds_bytes<kDirR, kDirNT>(kDirTC);
+    static std::once_flag attr_once;
+    std::call_once(attr_once, [&] {
+        (void)hipFuncSetAttribute(
+            reinterpret_cast<const void *>(&lcfir::fir_direct_f64_kernel<kDirR, kDirNT>),
+            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    });
+    hipLaunchKernelGGL((lcfir::fir_direct_f64_kernel<kDirR, kDirNT>), dim3((unsigned)gx, nch),
+                       dim3(kDirNT), lds, s, p);
+    LCFIR_HIP(hipGetLastError());
+    return LCFIR_OK;
+}
+
+int resolve_method(lcfir_ctx *ctx) {
+    if (ctx->method != LCFIR_METHOD_AUTO) return ctx->method;
+    return lcfir::fft_preferred(ctx->ntaps) ? LCFIR_METHOD_FFT : LCFIR_METHOD_DIRECT;
+}
+
+int ensure_fft(lcfir_ctx *ctx, hipStream_t s) {
+    std::lock_guard<std::mutex> lk(ctx->fft_mu);
+    if (ctx->fft.ready) return LCFIR_OK;
+    std::string err;
+    if (!lcfir::fft_plan_build(ctx->fft, ctx->d_taps, ctx->ntaps, s, err))
+        return fail(LCFIR_EDEVICE, "fft plan: %s", err.c_str());
+    return LCFIR_OK;
+}
+
+// Run the filter for outputs [start, end) of nch channels.  x/y geometry as
+// in DirectParams.
+int run_filter(lcfir_ctx *ctx, lcfir::DirectParams p, int nch, hipStream_t s) {
+    p.taps = ctx->d_taps;
+    p.ntaps = ctx->ntaps;
+    p.half = ctx->half;
+    const int m = resolve_method(ctx);
+    if (m == LCFIR_METHOD_FFT) {
+        int rc = ensure_fft(ctx, s);
+        if (rc) return rc;
+        std::string err;
+        if (!lcfir::fft_launch(ctx->fft, p, nch, s, err))
+            return fail(LCFIR_EDEVICE, "fft launch: %s", err.c_str());
+        return LCFIR_OK;
+    }
+    return launch_direct(p, nch, s);
+}
+
+bool ranges_overlap(const void *a, size_t an, const void *b, size_t bn) {
+    auto pa = reinterpret_cast<uintptr_t>(a), pb = reinterpret_cast<uintptr_t>(b);
+    return pa < pb + bn && pb < pa + an;
+}
+
+// ---- staging pool for the host-pointer entry point ------------------------
+struct Staging {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    float *d_x = nullptr;
+    size_t x_cap = 0;
+    float *d_y = nullptr;
+    size_t y_cap = 0;
+};
+
+std::mutex g_pool_mu;
+std::vector<Staging *> g_pool; // idle slots (process lifetime)
+
+Staging *borrow_staging(int device) {
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        for (size_t i = 0; i < g_pool.size(); ++i) {
+            if (g_pool[i]->device == device) {
+                Staging *s = g_pool[i];
+                g_pool.erase(g_pool.begin() + (long)i);
+                return s;
+            }
+        }
+    }
+    Staging *s = new Staging;
+    s->device = device;
+    if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete s;
+        return nullptr;
+    }
+    return s;
+}
+
+void return_staging(Staging *s) {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    g_pool.push_back(s);
+}
+
+int grow(float *&buf, size_t &cap, size_t need) {
+    if (cap >= need) return LCFIR_OK;
+    const size_t want = std::max(need, cap * 2);
+    if (buf) (void)hipFree(buf);
+    buf = nullptr;
+    cap = 0;
+    if (hipMalloc(reinterpret_cast<void **>(&buf), want * sizeof(float)) != hipSuccess)
+        return fail(LCFIR_ENOMEM, "hipMalloc(%zu floats) failed", want);
+    cap = want;
+    return LCFIR_OK;
+}
+
+inline unsigned *peak_bits(float *p) { return reinterpret_cast<unsigned *>(p); }
+
+int stream_blocks(int64_t n, int per_block_elems) {
+    int64_t b = (n + per_block_elems - 1) / per_block_elems;
+    return (int)std::max<int64_t>(1, std::min<int64_t>(b, 2048));
+}
+
+} // namespace
+
+extern "C" {
+
+int lcfir_abi_version(void) { return LCFIR_ABI_VERSION; }
+
+const char *lcfir_last_error(void) { return g_err.c_str(); }
+
+int lcfir_device_count(int *count) {
+    if (!count) return fail(LCFIR_EINVAL, "count is null");
+    int c = 0;
+    LCFIR_HIP(hipGetDeviceCount(&c));
+    *count = c;
+    return LCFIR_OK;
+}
+
+int lcfir_ctx_create(int device, const double *taps, int32_t ntaps, lcfir_ctx **out) {
+    if (!out) return fail(LCFIR_EINVAL, "out is null");
+    *out = nullptr;
+    if (!taps) return fail(LCFIR_EINVAL, "taps is null");
+    if (ntaps < 1 || (ntaps & 1) == 0)
+        return fail(LCFIR_EINVAL, "ntaps must be odd and >= 1 (kernel length M+1), got %d", ntaps);
+    int ndev = 0;
+    LCFIR_HIP(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev)
+        return fail(LCFIR_EINVAL, "device %d out of range (%d devices)", device, ndev);
+    DeviceGuard g(device);
+    if (!g.ok) return fail(LCFIR_EDEVICE, "hipSetDevice(%d) failed", device);
+    auto *ctx = new lcfir_ctx;
+    ctx->device = device;
+    ctx->ntaps = ntaps;
+    ctx->half = (ntaps - 1) / 2;
+    if (hipMalloc(reinterpret_cast<void **>(&ctx->d_taps), sizeof(double) * (size_t)ntaps) !=
+        hipSuccess) {
+        delete ctx;
+        return fail(LCFIR_ENOMEM, "hipMalloc for %d taps failed", ntaps);
+    }
+    if (hipMemcpy(ctx->d_taps, taps, sizeof(double) * (size_t)ntaps, hipMemcpyHostToDevice) !=
+        hipSuccess) {
+        (void)hipFree(ctx->d_taps);
+        delete ctx;
+        return fail(LCFIR_EDEVICE, "tap upload failed");
+    }
+    *out = ctx;
+    return LCFIR_OK;
+}
+
+int lcfir_ctx_destroy(lcfir_ctx *ctx) {
+    if (!ctx) return LCFIR_OK;
+    DeviceGuard g(ctx->device);
+    (void)hipDeviceSynchronize();
+    lcfir::fft_plan_free(ctx->fft);
+    if (ctx->d_taps) (void)hipFree(ctx->d_taps);
+    delete ctx;
+    return LCFIR_OK;
+}
+
+int lcfir_ctx_set_method(lcfir_ctx *ctx, int method) {
+    if (!ctx) return fail(LCFIR_EINVAL, "ctx is null");
+    if (method < LCFIR_METHOD_AUTO || method > LCFIR_METHOD_FFT)
+        return fail(LCFIR_EINVAL, "unknown method %d", method);
+    ctx->method = method;
+    return LCFIR_OK;
+}
+
+int lcfir_ctx_get_method(const lcfir_ctx *ctx, int *method) {
+    if (!ctx || !method) return fail(LCFIR_EINVAL, "null argument");
+    *method = resolve_method(const_cast<lcfir_ctx *>(ctx));
+    return LCFIR_OK;
+}
+
+int lcfir_ctx_half(const lcfir_ctx *ctx, int32_t *half) {
+    if (!ctx || !half) return fail(LCFIR_EINVAL, "null argument");
+    *half = ctx->half;
+    return LCFIR_OK;
+}
+
+int lcfir_ctx_ntaps(const lcfir_ctx *ctx, int32_t *ntaps) {
+    if (!ctx || !ntaps) return fail(LCFIR_EINVAL, "null argument");
+    *ntaps = ctx->ntaps;
+    return LCFIR_OK;
+}
+
+int lcfir_apply_range(lcfir_ctx *ctx, const float *x, int64_t n, float *y, int64_t start,
+                      int64_t end, lcfir_progress_fn progress, void *user) {
+    if (!ctx || !x || !y) return fail(LCFIR_EINVAL, "null argument");
+    if (n < 0 || start < 0 || end < start || end > n)
+        return fail(LCFIR_EINVAL, "bad range [%lld, %lld) for n=%lld", (long long)start,
+                    (long long)end, (long long)n);
+    if (end == start) return LCFIR_OK;
+    const int64_t lo = std::max<int64_t>(0, start - ctx->half);
+    const int64_t hi = std::min<int64_t>(n, end + ctx->half);
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return fail(LCFIR_EDEVICE, "hipSetDevice(%d) failed", ctx->device);
+    Staging *st = borrow_staging(ctx->device);
+    if (!st) return fail(LCFIR_EDEVICE, "stream creation failed");
+    int rc = grow(st->d_x, st->x_cap, (size_t)(hi - lo));
+    if (!rc) rc = grow(st->d_y, st->y_cap, (size_t)(end - start));
+    if (!rc) {
+        if (hipMemcpyAsync(st->d_x, x + lo, sizeof(float) * (size_t)(hi - lo),
+                           hipMemcpyHostToDevice, st->stream) != hipSuccess)
+            rc = fail(LCFIR_EDEVICE, "H2D copy failed");
+    }
+    if (!rc) {
+        lcfir::DirectParams p{};
+        p.x = st->d_x;
+        p.x_lo = lo;
+        p.x_hi = hi;
+        p.x_stride = 0;
+        p.y = st->d_y;
+        p.y_lo = start;
+        p.y_stride = 0;
+        p.start = start;
+        p.end = end;
+        p.peak = nullptr;
+        rc = run_filter(ctx, p, 1, st->stream);
+    }
+    if (!rc) {
+        if (hipMemcpyAsync(y + start, st->d_y, sizeof(float) * (size_t)(end - start),
+                           hipMemcpyDeviceToHost, st->stream) != hipSuccess)
+            rc = fail(LCFIR_EDEVICE, "D2H copy failed");
+    }
+    if (!rc) {
+        hipError_t e = hipStreamSynchronize(st->stream);
+        if (e != hipSuccess) rc = fail(LCFIR_EDEVICE, "kernel failed: %s", hipGetErrorString(e));
+    }
+    return_staging(st);
+    if (!rc && progress) progress(user, (uint64_t)(end - start));
+    return rc;
+}
+
+int lcfir_apply_range_dev(lcfir_ctx *ctx, const float *d_x, int64_t n, float *d_y, int64_t start,
+                          int64_t end, void *stream) {
+    if (!ctx || !d_x || !d_y) return fail(LCFIR_EINVAL, "null argument");
+    if (n < 0 || start < 0 || end < start || end > n)
+        return fail(LCFIR_EINVAL, "bad range [%lld, %lld) for n=%lld", (long long)start,
+                    (long long)end, (long long)n);
+    if (end == start) return LCFIR_OK;
+    if (ranges_overlap(d_x, sizeof(float) * (size_t)n, d_y + start,
+                       sizeof(float) * (size_t)(end - start)))
+        return fail(LCFIR_EINVAL, "output range aliases the input channel");
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return fail(LCFIR_EDEVICE, "hipSetDevice(%d) failed", ctx->device);
+    lcfir::DirectParams p{};
+    p.x = d_x;
+    p.x_lo = 0;
+    p.x_hi = n;
+    p.y = d_y;
+    p.y_lo = 0;
+    p.start = start;
+    p.end = end;
+    return run_filter(ctx, p, 1, reinterpret_cast<hipStream_t>(stream));
+}
+
+int lcfir_filter_channels_dev(lcfir_ctx *ctx, const float *d_x, int64_t x_stride, int32_t nch,
+                              int64_t n, float *d_y, int64_t y_stride, float *d_peak,
+                              void *stream) {
+    if (!ctx || !d_x || !d_y) return fail(LCFIR_EINVAL, "null argument");
+    if (nch < 0 || n < 0) return fail(LCFIR_EINVAL, "negative size");
+    if (nch == 0 || n == 0) return LCFIR_OK;
+    if (nch > 1 && (x_stride < n || y_stride < n))
+        return fail(LCFIR_EINVAL, "channel stride smaller than channel length");
+    const size_t xb = sizeof(float) * (size_t)(x_stride * (nch - 1) + n);
+    const size_t yb = sizeof(float) * (size_t)(y_stride * (nch - 1) + n);
+    if (ranges_overlap(d_x, xb, d_y, yb)) return fail(LCFIR_EINVAL, "d_y aliases d_x");
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return fail(LCFIR_EDEVICE, "hipSetDevice(%d) failed", ctx->device);
+    lcfir::DirectParams p{};
+    p.x = d_x;
+    p.x_lo = 0;
+    p.x_hi = n;
+    p.x_stride = x_stride;
+    p.y = d_y;
+    p.y_lo = 0;
+    p.y_stride = y_stride;
+    p.start = 0;
+    p.end = n;
+    p.peak = d_peak ? peak_bits(d_peak) : nullptr;
+    return run_filter(ctx, p, nch, reinterpret_cast<hipStream_t>(stream));
+}
+
+int lcfir_peak_reset_dev(float *d_peak, int32_t count, void *stream) {
+    if (!d_peak || count < 0) return fail(LCFIR_EINVAL, "bad peak buffer");
+    LCFIR_HIP(hipMemsetAsync(d_peak, 0, sizeof(float) * (size_t)count,
+                             reinterpret_cast<hipStream_t>(stream)));
+    return LCFIR_OK;
+}
+
+int lcfir_peak_dev(const float *d_y, int64_t stride, int32_t nch, int64_t n, float *d_peak,
+                   void *stream) {
+    if (!d_y || !d_peak || nch < 0 || n < 0) return fail(LCFIR_EINVAL, "bad argument");
+    if (nch == 0 || n == 0) return LCFIR_OK;
+    if (nch > 65535) return fail(LCFIR_EINVAL, "too many channels");
+    const int blocks = stream_blocks(n, 256 * 16);
+    hipLaunchKernelGGL(lcfir::peak_kernel, dim3(blocks, nch), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), d_y, stride, n, peak_bits(d_peak));
+    LCFIR_HIP(hipGetLastError());
+    return LCFIR_OK;
+}
+
+int lcfir_normalize_dev(float *d_y, int64_t stride, int32_t nch, int64_t n, const float *d_peak,
+                        int32_t npeak, int force, void *stream) {
+    if (!d_y || !d_peak || nch < 0 || n < 0 || npeak < 1)
+        return fail(LCFIR_EINVAL, "bad argument");
+    if (nch == 0 || n == 0) return LCFIR_OK;
+    if (nch > 65535) return fail(LCFIR_EINVAL, "too many channels");
+    const int blocks = stream_blocks(n, 256 * 16);
+    hipLaunchKernelGGL(lcfir::normalize_kernel, dim3(blocks, nch), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), d_y, stride, n,
+                       reinterpret_cast<const unsigned *>(d_peak), npeak, force);
+    LCFIR_HIP(hipGetLastError());
+    return LCFIR_OK;
+}
+
+int lcfir_channel_peak(int device, const float *y, int64_t n, float *peak) {
+    if (!y || !peak || n < 0) return fail(LCFIR_EINVAL, "bad argument");
+    *peak = 0.0f;
+    if (n == 0) return LCFIR_OK;
+    DeviceGuard g(device);
+    if (!g.ok) return fail(LCFIR_EDEVICE, "hipSetDevice(%d) failed", device);
+    Staging *st = borrow_staging(device);
+    if (!st) return fail(LCFIR_EDEVICE, "stream creation failed");
+    int rc = grow(st->d_x, st->x_cap, (size_t)n);
+    if (!rc) rc = grow(st->d_y, st->y_cap, 1);
+    if (!rc && hipMemcpyAsync(st->d_x, y, sizeof(float) * (size_t)n, hipMemcpyHostToDevice,
+                              st->stream) != hipSuccess)
+        rc = fail(LCFIR_EDEVICE, "H2D copy failed");
+    if (!rc) rc = lcfir_peak_reset_dev(st->d_y, 1, st->stream);
+    if (!rc) rc = lcfir_peak_dev(st->d_x, n, 1, n, st->d_y, st->stream);
+    if (!rc && hipMemcpyAsync(peak, st->d_y, sizeof(float), hipMemcpyDeviceToHost, st->stream) !=
+                   hipSuccess)
+        rc = fail(LCFIR_EDEVICE, "D2H copy failed");
+    if (!rc && hipStreamSynchronize(st->stream) != hipSuccess)
+        rc = fail(LCFIR_EDEVICE, "peak kernel failed");
+    return_staging(st);
+    return rc;
+}
+
+int lcfir_dev_malloc(int device, size_t bytes, void **out) {
+    if (!out) return fail(LCFIR_EINVAL, "out is null");
+    *out = nullptr;
+    DeviceGuard g(device);
+    if (!g.ok) return fail(LCFIR_EDEVICE, "hipSetDevice(%d) failed", device);
+    if (hipMalloc(out, bytes ? bytes : 1) != hipSuccess)
+        return fail(LCFIR_ENOMEM, "hipMalloc(%zu) failed", bytes);
+    return LCFIR_OK;
+}
+
+int lcfir_dev_free(void *p) {
+    if (p) LCFIR_HIP(hipFree(p));
+    return LCFIR_OK;
+}
+
+int lcfir_memcpy_h2d(void *dst, const void *src, size_t bytes, void *stream) {
+    if (!bytes) return LCFIR_OK;
+    if (!dst || !src) return fail(LCFIR_EINVAL, "null argument");
+    LCFIR_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice,
+                             reinterpret_cast<hipStream_t>(stream)));
+    return LCFIR_OK;
+}
+
+int lcfir_memcpy_d2h(void *dst, const void *src, size_t bytes, void *stream) {
+    if (!bytes) return LCFIR_OK;
+    if (!dst || !src) return fail(LCFIR_EINVAL, "null argument");
+    LCFIR_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost,
+                             reinterpret_cast<hipStream_t>(stream)));
+    LCFIR_HIP(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));
+    return LCFIR_OK;
+}
+
+int lcfir_stream_create(int device, void **stream) {
+    if (!stream) return fail(LCFIR_EINVAL, "stream is null");
+    DeviceGuard g(device);
+    if (!g.ok) return fail(LCFIR_EDEVICE, "hipSetDevice(%d) failed", device);
+    hipStream_t s = nullptr;
+    LCFIR_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    *stream = s;
+    return LCFIR_OK;
+}
+
+int lcfir_stream_destroy(void *stream) {
+    if (stream) LCFIR_HIP(hipStreamDestroy(reinterpret_cast<hipStream_t>(stream)));
+    return LCFIR_OK;
+}
+
+int lcfir_stream_sync(void *stream) {
+    LCFIR_HIP(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));
+    return LCFIR_OK;
+}
+
+} // extern "C"

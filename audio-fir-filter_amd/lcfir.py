@@ -1,0 +1,348 @@
+"""ctypes binding of the C ABI in include/lcfir.h (liblcfir.so).
+
+The product is the C ABI and its HIP kernels; this module is the thin
+Python-side binding used by bench.py, the tests and smoke().  It never
+computes a filtered sample itself and has no CPU fallback: if liblcfir.so is
+missing, or the device cannot run it, every call raises LcfirError.
+
+Reference interface mirrored (diskerror/audio-fir-filter):
+  Filter(...)                  ~ WindowedSinc<float64_t> as seen by the hot path
+                                 (ProcessFile.cp:47-50, FilterCore.h:29 getMo2)
+  apply_filter_range(...)      ~ FilterCore.h:20-79, same argument meaning
+  filter_channel(...)          ~ the per-channel chunk hand-off, ProcessFile.cp:57-87
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import threading
+from typing import Callable, Optional
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+REPO_ROOT = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(_HERE, "liblcfir.so")
+HEADER_PATH = os.path.join(REPO_ROOT, "include", "lcfir.h")
+
+METHOD_AUTO, METHOD_DIRECT, METHOD_FFT = 0, 1, 2
+METHODS = {"auto": METHOD_AUTO, "direct": METHOD_DIRECT, "fft": METHOD_FFT}
+
+OK, EINVAL, EDEVICE, ENOMEM, EINTERNAL = 0, 1, 2, 3, 4
+
+
+class LcfirError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"lcfir error {code}: {msg}")
+        self.code = code
+
+
+PROGRESS_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64)
+
+_c_int, _c_i32, _c_i64 = ctypes.c_int, ctypes.c_int32, ctypes.c_int64
+_vp, _fp, _dp = ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_double)
+_ctxp = ctypes.c_void_p
+
+_SIGNATURES = {
+    "lcfir_abi_version": ([], _c_int),
+    "lcfir_last_error": ([], ctypes.c_char_p),
+    "lcfir_device_count": ([ctypes.POINTER(_c_int)], _c_int),
+    "lcfir_ctx_create": ([_c_int, _dp, _c_i32, ctypes.POINTER(_ctxp)], _c_int),
+    "lcfir_ctx_destroy": ([_ctxp], _c_int),
+    "lcfir_ctx_set_method": ([_ctxp, _c_int], _c_int),
+    "lcfir_ctx_get_method": ([_ctxp, ctypes.POINTER(_c_int)], _c_int),
+    "lcfir_ctx_half": ([_ctxp, ctypes.POINTER(_c_i32)], _c_int),
+    "lcfir_ctx_ntaps": ([_ctxp, ctypes.POINTER(_c_i32)], _c_int),
+    "lcfir_apply_range": ([_ctxp, _vp, _c_i64, _vp, _c_i64, _c_i64, PROGRESS_FN, _vp], _c_int),
+    "lcfir_apply_range_dev": ([_ctxp, _vp, _c_i64, _vp, _c_i64, _c_i64, _vp], _c_int),
+    "lcfir_filter_channels_dev": (
+        [_ctxp, _vp, _c_i64, _c_i32, _c_i64, _vp, _c_i64, _vp, _vp], _c_int),
+    "lcfir_peak_reset_dev": ([_vp, _c_i32, _vp], _c_int),
+    "lcfir_peak_dev": ([_vp, _c_i64, _c_i32, _c_i64, _vp, _vp], _c_int),
+    "lcfir_normalize_dev": ([_vp, _c_i64, _c_i32, _c_i64, _vp, _c_i32, _c_int, _vp], _c_int),
+    "lcfir_channel_peak": ([_c_int, _vp, _c_i64, ctypes.POINTER(ctypes.c_float)], _c_int),
+    "lcfir_dev_malloc": ([_c_int, ctypes.c_size_t, ctypes.POINTER(_vp)], _c_int),
+    "lcfir_dev_free": ([_vp], _c_int),
+    "lcfir_memcpy_h2d": ([_vp, _vp, ctypes.c_size_t, _vp], _c_int),
+    "lcfir_memcpy_d2h": ([_vp, _vp, ctypes.c_size_t, _vp], _c_int),
+    "lcfir_stream_create": ([_c_int, ctypes.POINTER(_vp)], _c_int),
+    "lcfir_stream_destroy": ([_vp], _c_int),
+    "lcfir_stream_sync": ([_vp], _c_int),
+}
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def header_symbols(path: str = HEADER_PATH) -> list:
+    """Every function the C header declares (used by the export test)."""
+    text = open(path).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(lcfir_\w+)\s*\(", text, re.M)))
+
+
+def load(path: str = LIB_PATH):
+    """Load liblcfir.so.  Raises LcfirError if it has not been built."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise LcfirError(EINTERNAL, f"{path} is missing: build it with "
+                             "`python -c 'import __graft_entry__ as g; g.build()'`")
+        lib = ctypes.CDLL(path)
+        for name, (argtypes, restype) in _SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.argtypes = argtypes
+            fn.restype = restype
+        if lib.lcfir_abi_version() != 1:
+            raise LcfirError(EINTERNAL, "ABI version mismatch")
+        _lib = lib
+        return lib
+
+
+def _check(rc: int):
+    if rc != OK:
+        msg = _lib.lcfir_last_error()
+        raise LcfirError(rc, msg.decode() if msg else "")
+
+
+def device_count() -> int:
+    lib = load()
+    c = ctypes.c_int(0)
+    _check(lib.lcfir_device_count(ctypes.byref(c)))
+    return c.value
+
+
+def _ptr(a) -> int:
+    """Raw address of a numpy array or a torch tensor."""
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    if hasattr(a, "data_ptr"):
+        return a.data_ptr()
+    if isinstance(a, int):
+        return a
+    raise TypeError(f"cannot take the address of {type(a)}")
+
+
+class Filter:
+    """One filter (tap set) resident on one device.
+
+    Mirrors the reference's `WindowedSinc<float64_t>` as used by the hot path:
+    it holds the M+1 taps and answers getMo2() (`half`).
+    """
+
+    def __init__(self, taps, device: int = 0, method: str = "auto"):
+        lib = load()
+        t = np.ascontiguousarray(np.asarray(taps, dtype=np.float64))
+        self._taps = t
+        self.device = device
+        ctx = ctypes.c_void_p()
+        _check(lib.lcfir_ctx_create(device, t.ctypes.data_as(_dp), int(t.size), ctypes.byref(ctx)))
+        self._ctx = ctx
+        self.set_method(method)
+
+    @property
+    def ctx(self):
+        return self._ctx
+
+    def set_method(self, method: str):
+        _check(load().lcfir_ctx_set_method(self._ctx, METHODS[method]))
+
+    @property
+    def method(self) -> str:
+        m = ctypes.c_int()
+        _check(load().lcfir_ctx_get_method(self._ctx, ctypes.byref(m)))
+        return {v: k for k, v in METHODS.items()}[m.value]
+
+    @property
+    def half(self) -> int:
+        h = ctypes.c_int32()
+        _check(load().lcfir_ctx_half(self._ctx, ctypes.byref(h)))
+        return h.value
+
+    getMo2 = half
+
+    @property
+    def ntaps(self) -> int:
+        n = ctypes.c_int32()
+        _check(load().lcfir_ctx_ntaps(self._ctx, ctypes.byref(n)))
+        return n.value
+
+    @property
+    def taps(self) -> np.ndarray:
+        return self._taps
+
+    def close(self):
+        if self._ctx:
+            load().lcfir_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- host-pointer hot path (FilterCore.h:20-79) ------------------------
+    def apply_range(self, channel: np.ndarray, temp_output: np.ndarray, start: int, end: int,
+                    progress: Optional[Callable[[int], None]] = None):
+        if channel.dtype != np.float32 or temp_output.dtype != np.float32:
+            raise TypeError("channel and temp_output must be float32")
+        if not (channel.flags.c_contiguous and temp_output.flags.c_contiguous):
+            raise ValueError("arrays must be contiguous")
+        if temp_output.size < channel.size:
+            raise ValueError("temp_output shorter than channel")
+        cb = PROGRESS_FN(0) if progress is None else PROGRESS_FN(lambda _u, c: progress(int(c)))
+        _check(load().lcfir_apply_range(self._ctx, channel.ctypes.data, channel.size,
+                                        temp_output.ctypes.data, int(start), int(end), cb, None))
+
+    # -- device-pointer variants ---------------------------------------------
+    def apply_range_dev(self, d_x, n: int, d_y, start: int, end: int, stream=0):
+        _check(load().lcfir_apply_range_dev(self._ctx, _ptr(d_x), n, _ptr(d_y), start, end,
+                                            stream or None))
+
+    def filter_channels_dev(self, d_x, x_stride: int, nch: int, n: int, d_y, y_stride: int,
+                            d_peak=None, stream=0):
+        _check(load().lcfir_filter_channels_dev(
+            self._ctx, _ptr(d_x), x_stride, nch, n, _ptr(d_y), y_stride,
+            _ptr(d_peak) if d_peak is not None else None, stream or None))
+
+
+class ThreadSafeProgress:
+    """Counterpart of the reference's ThreadSafeProgress (ProgressBar.h:57-82):
+    an atomic counter fed by report(count) from several threads."""
+
+    def __init__(self, total: int):
+        self.total = total
+        self.count = 0
+        self._lock = threading.Lock()
+
+    def report(self, count: int):
+        with self._lock:
+            self.count += count
+
+
+def apply_filter_range(channel: np.ndarray, sinc: Filter, temp_output: np.ndarray,
+                       startIdx: int, endIdx: int, progress: Optional[ThreadSafeProgress] = None):
+    """Reference-signature mirror of apply_filter_range (FilterCore.h:20-27)."""
+    sinc.apply_range(channel, temp_output, startIdx, endIdx,
+                     None if progress is None else progress.report)
+
+
+def filter_channel(channel: np.ndarray, sinc: Filter, num_threads: int,
+                   progress: Optional[ThreadSafeProgress] = None) -> np.ndarray:
+    """The per-channel chunk hand-off of ProcessFile.cp:57-87: chunk =
+    N / num_threads, the last thread takes the remainder, every thread calls
+    apply_filter_range on its disjoint range, then join."""
+    n = channel.size
+    out = np.zeros(n, dtype=np.float32)
+    num_threads = max(1, int(num_threads))
+    chunk = n // num_threads
+    errors = []
+
+    def run(s, e):
+        try:
+            apply_filter_range(channel, sinc, out, s, e, progress)
+        except Exception as ex:  # surfaced after join
+            errors.append(ex)
+
+    threads = []
+    for i in range(num_threads):
+        s = i * chunk
+        e = n if i == num_threads - 1 else s + chunk
+        t = threading.Thread(target=run, args=(s, e))
+        t.start()
+        threads.append(t)
+    for t in threads:
+        t.join()
+    if errors:
+        raise errors[0]
+    return out
+
+
+# -- device post-pass helpers (ProcessFile.cp:91-101) ---------------------------
+def peak_reset_dev(d_peak, count: int, stream=0):
+    _check(load().lcfir_peak_reset_dev(_ptr(d_peak), count, stream or None))
+
+
+def peak_dev(d_y, stride: int, nch: int, n: int, d_peak, stream=0):
+    _check(load().lcfir_peak_dev(_ptr(d_y), stride, nch, n, _ptr(d_peak), stream or None))
+
+
+def normalize_dev(d_y, stride: int, nch: int, n: int, d_peak, npeak: int, force: bool, stream=0):
+    _check(load().lcfir_normalize_dev(_ptr(d_y), stride, nch, n, _ptr(d_peak), npeak,
+                                      1 if force else 0, stream or None))
+
+
+def channel_peak(y: np.ndarray, device: int = 0) -> float:
+    p = ctypes.c_float()
+    y = np.ascontiguousarray(y, dtype=np.float32)
+    _check(load().lcfir_channel_peak(device, y.ctypes.data, y.size, ctypes.byref(p)))
+    return p.value
+
+
+# -- device memory through the C ABI (no torch needed) -------------------------
+class DeviceBuffer:
+    """A device allocation made through lcfir_dev_malloc (HBM of `device`)."""
+
+    def __init__(self, nbytes: int, device: int = 0):
+        p = ctypes.c_void_p()
+        _check(load().lcfir_dev_malloc(device, int(nbytes), ctypes.byref(p)))
+        self.ptr = p.value
+        self.nbytes = int(nbytes)
+        self.device = device
+
+    @classmethod
+    def from_array(cls, a: np.ndarray, device: int = 0) -> "DeviceBuffer":
+        a = np.ascontiguousarray(a)
+        b = cls(a.nbytes, device)
+        b.upload(a)
+        return b
+
+    def upload(self, a: np.ndarray, stream=0):
+        a = np.ascontiguousarray(a)
+        assert a.nbytes <= self.nbytes
+        _check(load().lcfir_memcpy_h2d(self.ptr, a.ctypes.data, a.nbytes, stream or None))
+        if not stream:
+            sync()
+
+    def download(self, shape, dtype=np.float32, stream=0) -> np.ndarray:
+        out = np.empty(shape, dtype=dtype)
+        assert out.nbytes <= self.nbytes
+        _check(load().lcfir_memcpy_d2h(out.ctypes.data, self.ptr, out.nbytes, stream or None))
+        return out
+
+    def data_ptr(self) -> int:
+        return self.ptr
+
+    def free(self):
+        if self.ptr:
+            load().lcfir_dev_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def sync(stream=0):
+    """Wait for `stream` (0 = the legacy default stream)."""
+    _check(load().lcfir_stream_sync(stream or None))
+
+
+def hip_runtimes() -> list:
+    """Paths of every libamdhip64 mapped into this process.  Device pointers
+    from torch are only valid here if this is a single runtime (import torch
+    before lcfir so the SONAME libamdhip64.so.7 resolves to torch's copy)."""
+    paths = set()
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                if "libamdhip64" in line:
+                    paths.add(os.path.realpath(line.split()[-1]))
+    except OSError:
+        pass
+    return sorted(paths)

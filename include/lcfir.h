@@ -1,0 +1,130 @@
+/*
+ * lcfir.h -- C ABI of the MI355X (gfx950) low-cut FIR hot path.
+ *
+ * This is the drop-in boundary for the reference's hot path
+ * (diskerror/audio-fir-filter, "lowcut"):
+ *
+ *   void apply_filter_range(const VectorMath<float32_t>& channel,
+ *                           const WindowedSinc<float64_t>& sinc,
+ *                           VectorMath<float32_t>& temp_output,
+ *                           int_fast64_t startIdx, int_fast64_t endIdx,
+ *                           ThreadSafeProgress* progress);      FilterCore.h:20-27
+ *
+ * called by N std::threads on disjoint [start,end) chunks of one channel
+ * (ProcessFile.cp:60-83), plus the per-file peak/normalize post-pass
+ * (ProcessFile.cp:91-101).  Every entry point below names the reference
+ * interface it replaces.  Plain C: no exceptions cross this boundary, every
+ * function returns an lcfir_status, and lcfir_last_error() holds a
+ * thread-local message for the last failure on the calling thread.
+ *
+ * Semantics of a filtered sample (zero-padded, centred linear convolution,
+ * output length = input length):
+ *     y[n] = (float) sum_{k=0}^{T-1} h[k] * x[n - M/2 + k],   x[i] = 0 outside [0, N)
+ * with T = M + 1 odd taps (WindowedSinc kernel length, getMo2() = M/2),
+ * f32 samples, f64 taps, f64 accumulation, one round-to-nearest-even to f32.
+ */
+#ifndef LCFIR_H
+#define LCFIR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LCFIR_ABI_VERSION 1
+
+typedef struct lcfir_ctx lcfir_ctx;
+
+typedef enum lcfir_status {
+    LCFIR_OK = 0,
+    LCFIR_EINVAL = 1,    /* bad argument (null pointer, even tap count, bad range) */
+    LCFIR_EDEVICE = 2,   /* HIP runtime / device error */
+    LCFIR_ENOMEM = 3,    /* device or host allocation failed */
+    LCFIR_EINTERNAL = 4
+} lcfir_status;
+
+/* How the convolution is evaluated.  All methods meet the same parity bar. */
+typedef enum lcfir_method {
+    LCFIR_METHOD_AUTO = 0,   /* fastest method for the tap count */
+    LCFIR_METHOD_DIRECT = 1, /* strict-order f64 FMA chain per output (bit-exact vs the
+                                oracle's ORACLE_FMA restatement) */
+    LCFIR_METHOD_FFT = 2     /* f64 overlap-save FFT convolution */
+} lcfir_method;
+
+/* Progress callback: `count` more samples finished.  Replaces
+ * ThreadSafeProgress::report(size_t) (ProgressBar.h:69-81). */
+typedef void (*lcfir_progress_fn)(void *user, uint64_t count);
+
+/* ---- library --------------------------------------------------------- */
+int lcfir_abi_version(void);
+const char *lcfir_last_error(void);
+int lcfir_device_count(int *count);
+
+/* ---- filter context ---------------------------------------------------- */
+/* Uploads the taps to `device` once.  Replaces the per-file construction of
+ * WindowedSinc<float64_t> (ProcessFile.cp:47-50) as seen by the hot path:
+ * taps = the kernel, ntaps = M + 1 (must be odd), half = getMo2()
+ * (FilterCore.h:29). */
+int lcfir_ctx_create(int device, const double *taps, int32_t ntaps, lcfir_ctx **out);
+int lcfir_ctx_destroy(lcfir_ctx *ctx);
+int lcfir_ctx_set_method(lcfir_ctx *ctx, int method);
+int lcfir_ctx_get_method(const lcfir_ctx *ctx, int *method);
+int lcfir_ctx_half(const lcfir_ctx *ctx, int32_t *half); /* getMo2() */
+int lcfir_ctx_ntaps(const lcfir_ctx *ctx, int32_t *ntaps);
+
+/* ---- the hot path: host-pointer range call ----------------------------- */
+/* Replaces apply_filter_range(channel, sinc, temp_output, startIdx, endIdx,
+ * progress) (FilterCore.h:20-79).  x: the whole channel (n samples, host);
+ * y: the caller's output buffer (n samples, host); only y[start, end) is
+ * written; x is read over [start - half, end + half) intersected with [0, n).
+ * Re-entrant: any number of host threads may call it concurrently on the
+ * same ctx with disjoint ranges (the ProcessFile.cp:71-78 pattern).
+ * progress may be NULL; otherwise it receives end - start once the range is
+ * done (the reference batches reports every 2048 samples, FilterCore.h:38-54). */
+int lcfir_apply_range(lcfir_ctx *ctx, const float *x, int64_t n, float *y, int64_t start,
+                      int64_t end, lcfir_progress_fn progress, void *user);
+
+/* ---- device-resident variants (async on a hipStream_t passed as void*) -- */
+/* Same as lcfir_apply_range with device pointers; no host synchronisation. */
+int lcfir_apply_range_dev(lcfir_ctx *ctx, const float *d_x, int64_t n, float *d_y,
+                          int64_t start, int64_t end, void *stream);
+
+/* The whole per-channel loop of ProcessFile.cp:57-87 for nch deinterleaved
+ * channels of n samples: channel c at d_x + c*x_stride, output at
+ * d_y + c*y_stride (d_y must not alias d_x).  If d_peak is non-NULL it must
+ * hold nch floats, zeroed by the caller (or by lcfir_peak_reset_dev); each
+ * receives max|y| of its channel (fused into the filter kernel). */
+int lcfir_filter_channels_dev(lcfir_ctx *ctx, const float *d_x, int64_t x_stride, int32_t nch,
+                              int64_t n, float *d_y, int64_t y_stride, float *d_peak,
+                              void *stream);
+
+/* ---- peak + normalize post-pass (ProcessFile.cp:91-101) ----------------- */
+/* max_mag() over each channel (VectorMath::max_mag); d_peak[c] = max(d_peak[c], max|y_c|). */
+int lcfir_peak_reset_dev(float *d_peak, int32_t count, void *stream);
+int lcfir_peak_dev(const float *d_y, int64_t stride, int32_t nch, int64_t n, float *d_peak,
+                   void *stream);
+/* Per-file normalize decision and rescale, device-side (no host sync):
+ * peak = max over d_peak[0..npeak); if (peak > 1 || force) every sample
+ * becomes (float)((double)y * (1.0 / (double)peak)).  The scale rule of
+ * c_lib's AudioSamples::normalize is unpinned. */
+int lcfir_normalize_dev(float *d_y, int64_t stride, int32_t nch, int64_t n,
+                        const float *d_peak, int32_t npeak, int force, void *stream);
+/* Host-pointer convenience: max|y| of one channel (VectorMath::max_mag). */
+int lcfir_channel_peak(int device, const float *y, int64_t n, float *peak);
+
+/* ---- device memory / stream helpers for hosts without a GPU runtime ----- */
+int lcfir_dev_malloc(int device, size_t bytes, void **out);
+int lcfir_dev_free(void *p);
+int lcfir_memcpy_h2d(void *dst, const void *src, size_t bytes, void *stream);
+int lcfir_memcpy_d2h(void *dst, const void *src, size_t bytes, void *stream);
+int lcfir_stream_create(int device, void **stream);
+int lcfir_stream_destroy(void *stream);
+int lcfir_stream_sync(void *stream);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* LCFIR_H */

@@ -1,0 +1,250 @@
+"""GPU parity: the HIP path, called through the C ABI, against the oracle.
+
+Bars (written here, used below):
+  * METHOD direct: bit-exact against the oracle's strict-order f64 FMA chain
+    (ORACLE_FMA) -- same accumulation order and rounding, so any difference is
+    a bug;
+  * every method: RMS(y_gpu - y_longdouble) <= 1e-9 in full-scale units
+    (BASELINE.json north_star), and at most 1 ulp(f32) per sample.
+"""
+import threading
+
+import numpy as np
+import pytest
+
+from conftest import golden_names, load_golden
+
+pytestmark = pytest.mark.gpu
+
+RMS_TOL = 1e-9
+METHODS = ["direct"]
+
+
+@pytest.fixture(scope="module")
+def lc():
+    import lcfir
+    assert lcfir.device_count() >= 1, "no GPU visible"
+    return lcfir
+
+
+def rms(a, b):
+    d = np.asarray(a, np.float64) - np.asarray(b, np.float64)
+    return float(np.sqrt(np.mean(d * d))) if d.size else 0.0
+
+
+def max_ulps(a, b):
+    a = np.asarray(a, np.float32)
+    b = np.asarray(b, np.float32)
+    ia = a.view(np.int32).astype(np.int64)
+    ib = b.view(np.int32).astype(np.int64)
+    ia = np.where(ia < 0, -(ia & 0x7FFFFFFF), ia)
+    ib = np.where(ib < 0, -(ib & 0x7FFFFFFF), ib)
+    return int(np.abs(ia - ib).max()) if a.size else 0
+
+
+def gpu_filter_channels(lc, flt, x):
+    """Run lcfir_filter_channels_dev on a [nch][n] host array; returns (y, peaks)."""
+    x = np.ascontiguousarray(x, np.float32)
+    nch, n = x.shape
+    dx = lc.DeviceBuffer.from_array(x)
+    dy = lc.DeviceBuffer(max(1, x.nbytes))
+    dpk = lc.DeviceBuffer(4 * nch)
+    lc.peak_reset_dev(dpk, nch)
+    flt.filter_channels_dev(dx, n, nch, n, dy, n, dpk)
+    lc.sync()
+    y = dy.download((nch, n))
+    pk = dpk.download(nch)
+    for b in (dx, dy, dpk):
+        b.free()
+    return y, pk
+
+
+@pytest.mark.parametrize("method", METHODS)
+@pytest.mark.parametrize("name", golden_names())
+def test_golden_vectors(lc, oracle_mod, name, method):
+    g = load_golden(name)
+    flt = lc.Filter(g["taps"], method=method)
+    y, pk = gpu_filter_channels(lc, flt, g["x"])
+    for c in range(g["x"].shape[0]):
+        assert rms(y[c], g["y"][c]) <= RMS_TOL
+        assert max_ulps(y[c], g["y"][c]) <= 1
+        if method == "direct":
+            ref = oracle_mod.filter_channel(g["x"][c], g["taps"], oracle_mod.MODE_FMA)
+            assert np.array_equal(y[c], ref), f"channel {c}: direct kernel not bit-exact"
+        assert pk[c] == np.abs(y[c]).max()
+
+
+@pytest.mark.parametrize("method", METHODS)
+@pytest.mark.parametrize("threads", [1, 2, 3, 8])
+def test_chunk_handoff_threads(lc, oracle_mod, method, threads):
+    """ProcessFile.cp:60-83: N host threads, disjoint [start,end), one channel."""
+    g = load_golden("random_int24")
+    flt = lc.Filter(g["taps"], method=method)
+    prog = lc.ThreadSafeProgress(g["x"].shape[1])
+    y = lc.filter_channel(g["x"][0], flt, threads, prog)
+    assert prog.count == g["x"].shape[1]
+    ref = oracle_mod.filter_channel(g["x"][0], g["taps"], oracle_mod.MODE_FMA)
+    if method == "direct":
+        assert np.array_equal(y, ref)
+    assert rms(y, g["y"][0]) <= RMS_TOL
+
+
+@pytest.mark.parametrize("method", METHODS)
+def test_apply_range_writes_only_its_range(lc, oracle_mod, method):
+    g = load_golden("ragged_taps")
+    x, taps = g["x"][0], g["taps"]
+    flt = lc.Filter(taps, method=method)
+    n = x.size
+    for (s, e) in [(0, 1), (0, 1955), (1954, 1957), (3000, 7000), (n - 5, n), (n, n), (17, 18)]:
+        y = np.full(n, np.float32(7.0))
+        lc.apply_filter_range(x, flt, y, s, e)
+        assert np.all(y[:s] == 7.0) and np.all(y[e:] == 7.0)
+        ref = oracle_mod.filter_channel(x, taps, oracle_mod.MODE_FMA)
+        if method == "direct":
+            assert np.array_equal(y[s:e], ref[s:e])
+        assert rms(y[s:e], g["y"][0][s:e]) <= RMS_TOL
+
+
+@pytest.mark.parametrize("method", METHODS)
+def test_apply_range_dev(lc, oracle_mod, method):
+    g = load_golden("float_source")
+    x, taps = g["x"][3], g["taps"]
+    flt = lc.Filter(taps, method=method)
+    n = x.size
+    dx = lc.DeviceBuffer.from_array(x)
+    dy = lc.DeviceBuffer.from_array(np.zeros(n, np.float32))
+    for (s, e) in [(0, 700), (700, 2999), (2999, 3000)]:
+        flt.apply_range_dev(dx, n, dy, s, e)
+    lc.sync()
+    y = dy.download(n)
+    assert rms(y, g["y"][3]) <= RMS_TOL
+    if method == "direct":
+        assert np.array_equal(y, oracle_mod.filter_channel(x, taps, oracle_mod.MODE_FMA))
+
+
+def test_concurrent_contexts_and_threads(lc, oracle_mod):
+    """Several filters used from several threads at once (re-entrancy)."""
+    g1, g2 = load_golden("random_int24"), load_golden("sine")
+    f1, f2 = lc.Filter(g1["taps"]), lc.Filter(g2["taps"])
+    out = {}
+
+    def job(key, flt, x):
+        out[key] = lc.filter_channel(x, flt, 3)
+
+    ts = [threading.Thread(target=job, args=(i, f, gg["x"][0]))
+          for i, (f, gg) in enumerate([(f1, g1), (f2, g2), (f1, g1), (f2, g2)])]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for i, gg in enumerate([g1, g2, g1, g2]):
+        assert rms(out[i], gg["y"][0]) <= RMS_TOL
+
+
+def test_errors_are_reported(lc):
+    flt = lc.Filter(np.ones(3))
+    x = np.zeros(10, np.float32)
+    y = np.zeros(10, np.float32)
+    with pytest.raises(lc.LcfirError) as e:
+        flt.apply_range(x, y, 5, 11)
+    assert e.value.code == lc.EINVAL
+    with pytest.raises(lc.LcfirError):
+        flt.apply_range(x, y, 6, 5)
+    d = lc.DeviceBuffer.from_array(np.zeros(100, np.float32))
+    with pytest.raises(lc.LcfirError) as e:  # in-place (aliasing) is rejected
+        flt.apply_range_dev(d, 100, d, 0, 100)
+    assert "alias" in str(e.value)
+    with pytest.raises(lc.LcfirError):
+        lc.Filter(np.ones(3), device=99)
+
+
+def test_empty_and_degenerate(lc):
+    flt = lc.Filter(np.array([2.0]))
+    y, pk = gpu_filter_channels(lc, flt, np.zeros((1, 0), np.float32))
+    assert y.size == 0
+    x = np.array([[0.25, -0.5, 1.0]], np.float32)
+    y, pk = gpu_filter_channels(lc, flt, x)
+    assert np.array_equal(y, 2 * x) and pk[0] == 2.0
+
+
+def test_peak_and_normalize_match_processfile(lc, oracle_mod):
+    """ProcessFile.cp:91-101 post-pass on the device vs the oracle."""
+    g = load_golden("random_int24")
+    flt = lc.Filter(g["taps"], method="direct")
+    for gain, force in [(1.0, False), (1.0, True), (3.0, False)]:
+        x = np.ascontiguousarray(g["x"] * np.float32(gain))
+        nch, n = x.shape
+        dx = lc.DeviceBuffer.from_array(x)
+        dy = lc.DeviceBuffer(x.nbytes)
+        dpk = lc.DeviceBuffer(4 * nch)
+        lc.peak_reset_dev(dpk, nch)
+        flt.filter_channels_dev(dx, n, nch, n, dy, n, dpk)
+        lc.normalize_dev(dy, n, nch, n, dpk, nch, force)
+        lc.sync()
+        y = dy.download((nch, n))
+        ref = x.copy()
+        peak = oracle_mod.process_buffer(ref, g["taps"], nthreads=2, normalize=force)
+        assert np.array_equal(y, ref), (gain, force)
+        assert np.isclose(dpk.download(nch).max(), peak, rtol=0, atol=0)
+        # standalone peak kernel agrees with the fused one
+        dpk2 = lc.DeviceBuffer(4 * nch)
+        lc.peak_reset_dev(dpk2, nch)
+        flt.filter_channels_dev(dx, n, nch, n, dy, n, None)
+        lc.peak_dev(dy, n, nch, n, dpk2)
+        lc.sync()
+        assert np.array_equal(dpk2.download(nch), dpk.download(nch))
+    assert lc.channel_peak(g["y"][0]) == np.abs(g["y"][0]).max()
+
+
+def _sample_positions(n, half, k, seed):
+    rng = np.random.default_rng(seed)
+    edges = np.r_[np.arange(0, min(n, half + 64)), np.arange(max(0, n - half - 64), n)]
+    rand = rng.integers(0, n, k)
+    blocks = np.r_[[4095, 4096, 4097, 8191, 8192]]
+    return np.unique(np.r_[edges, rand, blocks[blocks < n]])
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("method", METHODS)
+def test_config2_full_size(lc, oracle_mod, method):
+    """Config 2 at full size (10 min stereo 48 kHz int24, 4001 taps) through
+    filter_channels_dev; checked at every edge sample plus 4096 random positions
+    per channel against the oracle, and the fused peak against the output."""
+    import synth
+    fs, n, nch = 48000.0, 28_800_000, 2
+    taps = oracle_mod.design_lowcut(20.0, fs, oracle_mod.lowcut_ntaps(48.0, fs))
+    assert taps.size == 4001
+    x = synth.file_buffer(nch, n, fs, file=0, bits=24)
+    flt = lc.Filter(taps, method=method)
+    y, pk = gpu_filter_channels(lc, flt, x)
+    for c in range(nch):
+        idx = _sample_positions(n, 2000, 4096, 100 + c)
+        ref_ld, _ = oracle_mod.filter_points(x[c], taps, idx, oracle_mod.MODE_LD)
+        assert rms(y[c][idx], ref_ld) <= RMS_TOL
+        assert max_ulps(y[c][idx], ref_ld) <= 1
+        if method == "direct":
+            ref_fma, _ = oracle_mod.filter_points(x[c], taps, idx, oracle_mod.MODE_FMA)
+            assert np.array_equal(y[c][idx], ref_fma)
+        assert pk[c] == np.abs(y[c]).max()
+        assert np.isfinite(y[c]).all()
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("method", METHODS)
+def test_config3_full_size(lc, oracle_mod, method):
+    """Config 3: 8 channels x 96 kHz float32 (60 s), 8001 taps (LDS / long-kernel stress)."""
+    import synth
+    fs, n, nch = 96000.0, 5_760_000, 8
+    taps = oracle_mod.design_lowcut(20.0, fs, 8001)
+    x = synth.file_buffer(nch, n, fs, file=1, bits=None)
+    flt = lc.Filter(taps, method=method)
+    y, pk = gpu_filter_channels(lc, flt, x)
+    for c in range(nch):
+        idx = _sample_positions(n, 4000, 1024, 200 + c)
+        ref_ld, _ = oracle_mod.filter_points(x[c], taps, idx, oracle_mod.MODE_LD)
+        assert rms(y[c][idx], ref_ld) <= RMS_TOL
+        assert max_ulps(y[c][idx], ref_ld) <= 1
+        if method == "direct":
+            ref_fma, _ = oracle_mod.filter_points(x[c], taps, idx, oracle_mod.MODE_FMA)
+            assert np.array_equal(y[c][idx], ref_fma)
+        assert pk[c] == np.abs(y[c]).max()
