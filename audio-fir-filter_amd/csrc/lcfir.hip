@@ -251,6 +251,9 @@ int lcfir_ctx_set_method(lcfir_ctx *ctx, int method) {
     if (!ctx) return fail(LCFIR_EINVAL, "ctx is null");
     if (method < LCFIR_METHOD_AUTO || method > LCFIR_METHOD_FFT)
         return fail(LCFIR_EINVAL, "unknown method %d", method);
+    if (method == LCFIR_METHOD_FFT && !lcfir::fft_supported(ctx->ntaps))
+        return fail(LCFIR_EINVAL, "FFT method supports at most %d taps (got %d)",
+                    lcfir::kFftL - lcfir::kFftMinB + 1, ctx->ntaps);
     ctx->method = method;
     return LCFIR_OK;
 }

@@ -140,7 +140,11 @@ class Filter:
         ctx = ctypes.c_void_p()
         _check(lib.lcfir_ctx_create(device, t.ctypes.data_as(_dp), int(t.size), ctypes.byref(ctx)))
         self._ctx = ctx
-        self.set_method(method)
+        try:
+            self.set_method(method)
+        except Exception:
+            self.close()
+            raise
 
     @property
     def ctx(self):

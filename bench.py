@@ -238,10 +238,10 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 6),
                 "traffic": traffic,
-                "kernel": "fir_direct_f64_kernel" if method == "direct" else "fir_fft_*",
+                "kernel": "fir_direct_f64_kernel" if method == "direct" else "fir_fft_f64_kernel",
                 "kernel_ms": round(kern_ms, 4),
                 "bytes_per_unit": 4,
-                "binding": "fp64-valu" if method == "direct" else "lds/hbm",
+                "binding": "fp64-valu",
                 "fp64_tflops": round(fp64_tflops, 3),
                 "fp64_frac": round(fp64_tflops / FP64_PEAK_TFLOPS, 4),
             },

@@ -19,7 +19,7 @@ step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step pytest_gpu 1200 python -m pytest tests -m gpu -x -q
 step bench 600 python bench.py --steps 10 --warmup 2 "$@"
 cd /tmp && export TMPDIR=/tmp
-step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench -- \
+step rocprof 600 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof" -o bench -- \
     python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline "$@"
 find "$OUT/prof" -name "*kernel_stats*" -exec cp {} "$OUT/" \;
 echo "== done"

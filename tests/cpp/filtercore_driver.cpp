@@ -1,0 +1,77 @@
+// Test driver for the C++ drop-in headers (include/lcfir/FilterCore.hpp,
+// ProcessBuffer.hpp).  Reads a raw float32 [nch][n] buffer and float64 taps,
+// runs the reference-structured process_buffer (threads calling
+// apply_filter_range with the FilterCore.h signature) or the device-resident
+// variant, writes the raw float32 result and prints "peak <value>".
+//
+// usage: filtercore_driver in.f32 taps.f64 out.f32 nch n threads mode normalize
+//        mode 0 = process_buffer (threaded hand-off), 1 = process_buffer_device
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <vector>
+
+#include "lcfir/ProcessBuffer.hpp"
+
+// Stand-in for c_lib's WindowedSinc<float64_t>: the drop-in only needs the taps.
+struct WindowedSinc {
+    std::vector<double> k;
+    const double *data() const { return k.data(); }
+    size_t size() const { return k.size(); }
+};
+
+// Counterpart of ThreadSafeProgress (ProgressBar.h:57-82).
+struct Progress {
+    std::mutex mu;
+    size_t count = 0;
+    void report(size_t c) {
+        std::lock_guard<std::mutex> lk(mu);
+        count += c;
+    }
+};
+
+template <class T>
+static std::vector<T> read_all(const char *path) {
+    std::ifstream f(path, std::ios::binary | std::ios::ate);
+    if (!f) { std::fprintf(stderr, "cannot open %s\n", path); std::exit(2); }
+    const size_t bytes = (size_t)f.tellg();
+    std::vector<T> v(bytes / sizeof(T));
+    f.seekg(0);
+    f.read(reinterpret_cast<char *>(v.data()), (std::streamsize)bytes);
+    return v;
+}
+
+int main(int argc, char **argv) {
+    if (argc != 9) {
+        std::fprintf(stderr, "usage: %s in.f32 taps.f64 out.f32 nch n threads mode normalize\n", argv[0]);
+        return 2;
+    }
+    const auto x = read_all<float>(argv[1]);
+    WindowedSinc sinc{read_all<double>(argv[2])};
+    const size_t nch = std::strtoul(argv[4], nullptr, 10), n = std::strtoul(argv[5], nullptr, 10);
+    lcfir::FilterOptions opts;
+    opts.num_threads = (unsigned)std::strtoul(argv[6], nullptr, 10);
+    const int mode = std::atoi(argv[7]);
+    opts.normalize = std::atoi(argv[8]) != 0;
+    if (x.size() != nch * n) { std::fprintf(stderr, "size mismatch\n"); return 2; }
+    std::vector<std::vector<float>> buf(nch);
+    for (size_t c = 0; c < nch; ++c) buf[c].assign(x.begin() + (long)(c * n), x.begin() + (long)((c + 1) * n));
+    float peak;
+    Progress prog;
+    try {
+        if (mode == 0) {
+            peak = lcfir::process_buffer(buf, sinc, opts, &prog);
+            if (prog.count != nch * n) { std::fprintf(stderr, "progress %zu\n", prog.count); return 3; }
+        } else {
+            lcfir::Filter flt(sinc.data(), (int32_t)sinc.size());
+            peak = lcfir::process_buffer_device(buf, flt, opts);
+        }
+    } catch (const lcfir::Error &e) {
+        std::fprintf(stderr, "lcfir error %d: %s\n", e.code(), e.what());
+        return 4;
+    }
+    std::ofstream o(argv[3], std::ios::binary);
+    for (auto &c : buf) o.write(reinterpret_cast<const char *>(c.data()), (std::streamsize)(c.size() * sizeof(float)));
+    std::printf("peak %.9g\n", (double)peak);
+    return 0;
+}

@@ -18,7 +18,21 @@ from conftest import golden_names, load_golden
 pytestmark = pytest.mark.gpu
 
 RMS_TOL = 1e-9
-METHODS = ["direct"]
+METHODS = ["direct", "fft"]
+# Golden cases whose exact outputs sit ON f32 rounding ties (taps with few
+# significant bits: 0.75 * x needs 26 bits).  Any method that is not exact in
+# f64 (the FFT: error ~1e-16) may round those ties either way; AUTO uses the
+# direct method for such filters (short tap counts).
+TIE_PRONE = {"single_tap"}
+
+
+def is_f32_tie(v):
+    """True if the f64 value v lies exactly half-way between two f32 values."""
+    a = np.float32(v)
+    if float(a) == v:
+        return False
+    b = np.nextafter(a, np.float32(np.inf) if v > float(a) else np.float32(-np.inf))
+    return 2.0 * v == float(a) + float(b)
 
 
 @pytest.fixture(scope="module")
@@ -47,6 +61,16 @@ def max_ulps(a, b, floor=1e-12):
     return int(d.max()) if a.size else 0
 
 
+def make_filter(lc, taps, method):
+    """Filter with the requested method; skip if the method cannot take this tap count."""
+    try:
+        return lc.Filter(taps, method=method)
+    except lc.LcfirError as e:
+        if method != "direct" and e.code == lc.EINVAL:
+            pytest.skip(f"{method} does not support {len(taps)} taps")
+        raise
+
+
 def gpu_filter_channels(lc, flt, x):
     """Run lcfir_filter_channels_dev on a [nch][n] host array; returns (y, peaks)."""
     x = np.ascontiguousarray(x, np.float32)
@@ -68,11 +92,16 @@ def gpu_filter_channels(lc, flt, x):
 @pytest.mark.parametrize("name", golden_names())
 def test_golden_vectors(lc, oracle_mod, name, method):
     g = load_golden(name)
-    flt = lc.Filter(g["taps"], method=method)
+    flt = make_filter(lc, g["taps"], method)
     y, pk = gpu_filter_channels(lc, flt, g["x"])
     for c in range(g["x"].shape[0]):
-        assert rms(y[c], g["y"][c]) <= RMS_TOL
         assert max_ulps(y[c], g["y"][c]) <= 1
+        if method == "fft" and name in TIE_PRONE:
+            # every mismatch must be an exact f32 rounding tie of the exact sum
+            bad = np.nonzero(y[c] != g["y"][c])[0]
+            assert all(is_f32_tie(g["y64"][c][i]) for i in bad)
+        else:
+            assert rms(y[c], g["y"][c]) <= RMS_TOL
         if method == "direct":
             ref = oracle_mod.filter_channel(g["x"][c], g["taps"], oracle_mod.MODE_FMA)
             assert np.array_equal(y[c], ref), f"channel {c}: direct kernel not bit-exact"
@@ -84,7 +113,7 @@ def test_golden_vectors(lc, oracle_mod, name, method):
 def test_chunk_handoff_threads(lc, oracle_mod, method, threads):
     """ProcessFile.cp:60-83: N host threads, disjoint [start,end), one channel."""
     g = load_golden("random_int24")
-    flt = lc.Filter(g["taps"], method=method)
+    flt = make_filter(lc, g["taps"], method)
     prog = lc.ThreadSafeProgress(g["x"].shape[1])
     y = lc.filter_channel(g["x"][0], flt, threads, prog)
     assert prog.count == g["x"].shape[1]
@@ -98,7 +127,7 @@ def test_chunk_handoff_threads(lc, oracle_mod, method, threads):
 def test_apply_range_writes_only_its_range(lc, oracle_mod, method):
     g = load_golden("ragged_taps")
     x, taps = g["x"][0], g["taps"]
-    flt = lc.Filter(taps, method=method)
+    flt = make_filter(lc, taps, method)
     n = x.size
     for (s, e) in [(0, 1), (0, 1955), (1954, 1957), (3000, 7000), (n - 5, n), (n, n), (17, 18)]:
         y = np.full(n, np.float32(7.0))
@@ -114,7 +143,7 @@ def test_apply_range_writes_only_its_range(lc, oracle_mod, method):
 def test_apply_range_dev(lc, oracle_mod, method):
     g = load_golden("float_source")
     x, taps = g["x"][3], g["taps"]
-    flt = lc.Filter(taps, method=method)
+    flt = make_filter(lc, taps, method)
     n = x.size
     dx = lc.DeviceBuffer.from_array(x)
     dy = lc.DeviceBuffer.from_array(np.zeros(n, np.float32))
@@ -220,7 +249,7 @@ def test_config2_full_size(lc, oracle_mod, method):
     taps = oracle_mod.design_lowcut(20.0, fs, oracle_mod.lowcut_ntaps(48.0, fs))
     assert taps.size == 4001
     x = synth.file_buffer(nch, n, fs, file=0, bits=24)
-    flt = lc.Filter(taps, method=method)
+    flt = make_filter(lc, taps, method)
     y, pk = gpu_filter_channels(lc, flt, x)
     for c in range(nch):
         idx = _sample_positions(n, 2000, 4096, 100 + c)
@@ -242,7 +271,7 @@ def test_config3_full_size(lc, oracle_mod, method):
     fs, n, nch = 96000.0, 5_760_000, 8
     taps = oracle_mod.design_lowcut(20.0, fs, 8001)
     x = synth.file_buffer(nch, n, fs, file=1, bits=None)
-    flt = lc.Filter(taps, method=method)
+    flt = make_filter(lc, taps, method)
     y, pk = gpu_filter_channels(lc, flt, x)
     for c in range(nch):
         idx = _sample_positions(n, 4000, 1024, 200 + c)
