@@ -1,0 +1,195 @@
+"""Multi-file, multi-GPU batch driver (BASELINE.json configs 4 and 5).
+
+The reference processes the files of a batch strictly one after another
+(main.cp:132-147), each through process_file (ProcessFile.cp:27-120).  Here
+one process per GPU takes a share of the batch:
+
+  * num_files >= world: whole files, round-robin -- "one file per GPU" when
+    num_files == world.  No data-path collective: files are independent.
+  * num_files < world: each file is split by sample range over a group of
+    ranks (each rank reads its range +- half the kernel, no halo exchange).
+    The per-file peak is then the max over the group: that is the one real
+    exchange step, a MAX all-reduce of the [num_files] peak vector (each
+    rank writes its own slots).  Over RCCL/xGMI it is a few dozen bytes.
+
+Normalize semantics follow the reference: per FILE (ProcessFile.cp:92-101,
+peak over the file's channels, rescale iff peak > 1 or --normalize).
+peak_scope="global" is the north-star config-5 variant (one peak over the
+whole batch, RCCL MAX all-reduce, every file rescaled by it) -- a deviation
+from the reference, offered only behind that explicit flag.
+
+Compute is pluggable (`Backend`): DeviceBackend runs the gfx950 kernels via
+the C ABI on torch-allocated HBM; tests plug a CPU backend built on the
+oracle to check the sharding and exchange logic with gloo.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable, Dict, List, Optional, Sequence
+
+
+@dataclass(frozen=True)
+class Shard:
+    file: int
+    start: int  # output range [start, end) of every channel of the file
+    end: int
+
+
+def plan_shards(nframes: Sequence[int], world: int) -> List[List[Shard]]:
+    """Shards per rank.  Files are whole when num_files >= world, otherwise
+    split into contiguous near-equal ranges over ranks (ProcessFile.cp:64-69
+    partition rule: chunk = n / parts, the last part takes the remainder)."""
+    nf = len(nframes)
+    out: List[List[Shard]] = [[] for _ in range(world)]
+    if nf == 0:
+        return out
+    if nf >= world:
+        for f, n in enumerate(nframes):
+            out[f % world].append(Shard(f, 0, int(n)))
+        return out
+    # nf < world: ranks [first_f, first_{f+1}) serve file f
+    base, extra = divmod(world, nf)
+    r = 0
+    for f, n in enumerate(nframes):
+        parts = base + (1 if f < extra else 0)
+        chunk = int(n) // parts
+        for i in range(parts):
+            s = i * chunk
+            e = int(n) if i == parts - 1 else s + chunk
+            out[r].append(Shard(f, s, e))
+            r += 1
+    return out
+
+
+def file_is_split(plan: List[List[Shard]]) -> bool:
+    owners: Dict[int, int] = {}
+    for rank, shards in enumerate(plan):
+        for sh in shards:
+            if owners.setdefault(sh.file, rank) != rank:
+                return True
+    return False
+
+
+def window(sh: Shard, n: int, half: int):
+    """Samples [x_lo, x_hi) a shard's outputs read (FilterCore.h:56-76)."""
+    return max(0, sh.start - half), min(n, sh.end + half)
+
+
+class Backend:
+    """Compute interface the driver needs (device or test CPU)."""
+
+    def upload(self, file: int, xw, x_lo: int, x_hi: int):  # -> handle
+        raise NotImplementedError
+
+    def alloc_out(self, nch: int, count: int):  # -> handle
+        raise NotImplementedError
+
+    def filter(self, xw, x_lo, x_hi, n, nch, yw, start, end, peaks, slot: int):
+        """outputs [start, end) into yw; max|y| over the shard's channels into peaks[slot]."""
+        raise NotImplementedError
+
+    def zero_peaks(self, peaks):
+        raise NotImplementedError
+
+    def normalize(self, yw, nch, count, peaks, slot: Optional[int], force: bool):
+        """rescale by 1/peak iff peak > 1 or force; slot None = max over all slots."""
+        raise NotImplementedError
+
+    def new_peaks(self, nfiles: int):
+        raise NotImplementedError
+
+
+class BatchRunner:
+    """One rank's share of a batch.  prepare() uploads the rank's sample
+    windows (untimed); step() is the timed per-batch compute: filter every
+    shard with fused peaks, exchange peaks if needed, normalize."""
+
+    def __init__(self, backend: Backend, rank: int, world: int, nframes: Sequence[int], nch: int,
+                 half: int, normalize: bool = False, peak_scope: str = "file",
+                 allreduce_max: Optional[Callable] = None):
+        if peak_scope not in ("file", "global"):
+            raise ValueError("peak_scope must be 'file' or 'global'")
+        self.b = backend
+        self.rank, self.world = rank, world
+        self.nframes = [int(n) for n in nframes]
+        self.nch, self.half = nch, half
+        self.normalize = normalize
+        self.scope = peak_scope
+        self.plan = plan_shards(self.nframes, world)
+        self.shards = self.plan[rank]
+        split = file_is_split(self.plan)
+        # the collective is needed only where files share ranks, or for the
+        # batch-global variant; per-file peaks of whole files stay local
+        self.exchange = (split or peak_scope == "global") and world > 1
+        if self.exchange and allreduce_max is None:
+            raise ValueError("this plan needs a MAX all-reduce of the peak vector")
+        self.allreduce_max = allreduce_max
+        self.peaks = backend.new_peaks(len(self.nframes))
+        self.inputs = []
+        self.outputs = []
+
+    def prepare(self, get_window: Callable):
+        """get_window(file, x_lo, x_hi) -> [nch][x_hi - x_lo] float32 samples."""
+        self.inputs, self.outputs = [], []
+        for sh in self.shards:
+            n = self.nframes[sh.file]
+            lo, hi = window(sh, n, self.half)
+            self.inputs.append((self.b.upload(sh.file, get_window(sh.file, lo, hi), lo, hi), lo, hi))
+            self.outputs.append(self.b.alloc_out(self.nch, sh.end - sh.start))
+
+    def step(self):
+        self.b.zero_peaks(self.peaks)
+        for sh, (xw, lo, hi), yw in zip(self.shards, self.inputs, self.outputs):
+            self.b.filter(xw, lo, hi, self.nframes[sh.file], self.nch, yw, sh.start, sh.end,
+                          self.peaks, sh.file)
+        if self.exchange:
+            self.allreduce_max(self.peaks)
+        for sh, yw in zip(self.shards, self.outputs):
+            slot = None if self.scope == "global" else sh.file
+            self.b.normalize(yw, self.nch, sh.end - sh.start, self.peaks, slot, self.normalize)
+
+    def results(self):
+        """[(shard, output handle)] for this rank."""
+        return list(zip(self.shards, self.outputs))
+
+
+class DeviceBackend(Backend):
+    """gfx950 kernels through the C ABI on torch-allocated HBM (one stream)."""
+
+    def __init__(self, flt, device):
+        import torch
+        import lcfir
+        self.torch, self.lc, self.flt, self.dev = torch, lcfir, flt, device
+        self.stream = torch.cuda.current_stream(device)
+        self.sp = self.stream.cuda_stream
+
+    def new_peaks(self, nfiles):
+        return self.torch.zeros(max(1, nfiles), dtype=self.torch.float32, device=self.dev)
+
+    def upload(self, file, xw, x_lo, x_hi):
+        t = self.torch
+        return t.as_tensor(xw, dtype=t.float32).contiguous().to(self.dev)
+
+    def alloc_out(self, nch, count):
+        return self.torch.empty((nch, count), dtype=self.torch.float32, device=self.dev)
+
+    def zero_peaks(self, peaks):
+        self.lc.peak_reset_dev(peaks, peaks.numel(), self.sp)
+
+    def filter(self, xw, x_lo, x_hi, n, nch, yw, start, end, peaks, slot):
+        # every channel's max|y| is folded into the file's slot inside the kernel
+        self.flt.filter_window_dev(xw, x_lo, x_hi, xw.shape[1], n, nch, yw, start, yw.shape[1],
+                                   start, end, peaks[slot:slot + 1], self.sp, peak_stride=0)
+
+    def normalize(self, yw, nch, count, peaks, slot, force):
+        p = peaks if slot is None else peaks[slot:slot + 1]
+        self.lc.normalize_dev(yw, yw.shape[1], nch, count, p, p.numel(), force, self.sp)
+
+
+def torch_allreduce_max(group=None):
+    """MAX all-reduce over torch.distributed (RCCL for device tensors, gloo on CPU)."""
+    import torch.distributed as dist
+
+    def f(peaks):
+        dist.all_reduce(peaks, op=dist.ReduceOp.MAX, group=group)
+    return f

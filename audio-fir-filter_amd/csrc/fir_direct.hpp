@@ -43,7 +43,8 @@ struct DirectParams {
     int32_t half;
     int64_t start, end; // output range (global indices)
     int32_t tc;         // taps per LDS stage (multiple of 2R)
-    unsigned *peak;     // per-channel max|y| as float bits (nullable)
+    unsigned *peak;     // max|y| as float bits (nullable): channel c -> peak[c * peak_stride]
+    int64_t peak_stride;
 };
 
 template <int R>
@@ -125,7 +126,7 @@ __global__ __launch_bounds__(NT) void fir_direct_f64_kernel(DirectParams p) {
     if (p.peak) {
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
-        if ((tid & 63) == 0) atomicMax(p.peak + ch, __float_as_uint(m));
+        if ((tid & 63) == 0) atomicMax(p.peak + ch * p.peak_stride, __float_as_uint(m));
     }
 }
 

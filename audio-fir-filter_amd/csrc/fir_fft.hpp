@@ -329,7 +329,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     if (p.peak) {
 #pragma unroll
         for (int s = 32; s >= 1; s >>= 1) pk = fmaxf(pk, __shfl_xor(pk, s, 64));
-        if ((j & 63) == 0) atomicMax(p.peak + ch, __float_as_uint(pk));
+        if ((j & 63) == 0) atomicMax(p.peak + ch * p.peak_stride, __float_as_uint(pk));
     }
 }
 

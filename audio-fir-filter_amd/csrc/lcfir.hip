@@ -371,6 +371,45 @@ int lcfir_filter_channels_dev(lcfir_ctx *ctx, const float *d_x, int64_t x_stride
     p.start = 0;
     p.end = n;
     p.peak = d_peak ? peak_bits(d_peak) : nullptr;
+    p.peak_stride = 1;
+    return run_filter(ctx, p, nch, reinterpret_cast<hipStream_t>(stream));
+}
+
+int lcfir_filter_window_dev(lcfir_ctx *ctx, const float *d_xw, int64_t x_lo, int64_t x_hi,
+                            int64_t x_stride, int64_t n, int32_t nch, float *d_yw, int64_t y_lo,
+                            int64_t y_stride, int64_t start, int64_t end, float *d_peak,
+                            int64_t peak_stride, void *stream) {
+    if (!ctx || !d_xw || !d_yw) return fail(LCFIR_EINVAL, "null argument");
+    if (nch < 0 || n < 0 || start < 0 || end < start || end > n)
+        return fail(LCFIR_EINVAL, "bad range [%lld, %lld) for n=%lld", (long long)start,
+                    (long long)end, (long long)n);
+    if (nch == 0 || end == start) return LCFIR_OK;
+    const int64_t need_lo = std::max<int64_t>(0, start - ctx->half);
+    const int64_t need_hi = std::min<int64_t>(n, end + ctx->half);
+    if (x_lo < 0 || x_hi > n || x_lo > need_lo || x_hi < need_hi)
+        return fail(LCFIR_EINVAL,
+                    "window [%lld, %lld) does not cover the samples [%lld, %lld) the outputs need",
+                    (long long)x_lo, (long long)x_hi, (long long)need_lo, (long long)need_hi);
+    if (y_lo > start) return fail(LCFIR_EINVAL, "y_lo after start");
+    if (nch > 1 && (x_stride < x_hi - x_lo || y_stride < end - y_lo))
+        return fail(LCFIR_EINVAL, "channel stride smaller than the window");
+    const size_t xb = sizeof(float) * (size_t)(x_stride * (nch - 1) + (x_hi - x_lo));
+    const size_t yb = sizeof(float) * (size_t)(y_stride * (nch - 1) + (end - y_lo));
+    if (ranges_overlap(d_xw, xb, d_yw, yb)) return fail(LCFIR_EINVAL, "d_yw aliases d_xw");
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return fail(LCFIR_EDEVICE, "hipSetDevice(%d) failed", ctx->device);
+    lcfir::DirectParams p{};
+    p.x = d_xw;
+    p.x_lo = x_lo;
+    p.x_hi = x_hi;
+    p.x_stride = x_stride;
+    p.y = d_yw;
+    p.y_lo = y_lo;
+    p.y_stride = y_stride;
+    p.start = start;
+    p.end = end;
+    p.peak = d_peak ? peak_bits(d_peak) : nullptr;
+    p.peak_stride = peak_stride;
     return run_filter(ctx, p, nch, reinterpret_cast<hipStream_t>(stream));
 }
 

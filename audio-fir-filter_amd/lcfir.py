@@ -58,6 +58,9 @@ _SIGNATURES = {
     "lcfir_apply_range_dev": ([_ctxp, _vp, _c_i64, _vp, _c_i64, _c_i64, _vp], _c_int),
     "lcfir_filter_channels_dev": (
         [_ctxp, _vp, _c_i64, _c_i32, _c_i64, _vp, _c_i64, _vp, _vp], _c_int),
+    "lcfir_filter_window_dev": (
+        [_ctxp, _vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_i32, _vp, _c_i64, _c_i64, _c_i64, _c_i64,
+         _vp, _c_i64, _vp], _c_int),
     "lcfir_peak_reset_dev": ([_vp, _c_i32, _vp], _c_int),
     "lcfir_peak_dev": ([_vp, _c_i64, _c_i32, _c_i64, _vp, _vp], _c_int),
     "lcfir_normalize_dev": ([_vp, _c_i64, _c_i32, _c_i64, _vp, _c_i32, _c_int, _vp], _c_int),
@@ -211,6 +214,19 @@ class Filter:
         _check(load().lcfir_filter_channels_dev(
             self._ctx, _ptr(d_x), x_stride, nch, n, _ptr(d_y), y_stride,
             _ptr(d_peak) if d_peak is not None else None, stream or None))
+
+
+def _filter_window_dev(self, d_xw, x_lo: int, x_hi: int, x_stride: int, n: int, nch: int,
+                       d_yw, y_lo: int, y_stride: int, start: int, end: int, d_peak=None,
+                       stream=0, peak_stride: int = 1):
+    """lcfir_filter_window_dev: outputs [start, end) of channels of length n
+    from the sample window [x_lo, x_hi) (a file sharded by sample range)."""
+    _check(load().lcfir_filter_window_dev(
+        self._ctx, _ptr(d_xw), x_lo, x_hi, x_stride, n, nch, _ptr(d_yw), y_lo, y_stride,
+        start, end, _ptr(d_peak) if d_peak is not None else None, peak_stride, stream or None))
+
+
+Filter.filter_window_dev = _filter_window_dev
 
 
 class ThreadSafeProgress:

@@ -1,18 +1,24 @@
 """bench.py -- filtered Msamples/s of the low-cut FIR hot path on MI355X.
 
-Workload (BASELINE.json configs[1], "config 2"): one 10-minute stereo 48 kHz
-int24 file per GPU = 2 channels x 28 800 000 samples, 4001-tap low-cut
-(-f 20, M = 4000), synthetic samples (SURVEY.md s8d generator; no audio data
-exists in this pipeline), already resident in HBM when timing starts.
+Default workload (BASELINE.json configs[1], "config 2"): one 10-minute stereo
+48 kHz int24 file per GPU = 2 channels x 28 800 000 samples, 4001-tap
+low-cut (-f 20, M = 4000).  Samples are synthetic (SURVEY.md s8d generator;
+no audio data exists in this pipeline) and already resident in HBM when
+timing starts.
 
-One step = the whole per-file compute path of ProcessFile.cp:57-101 on the
-device: filter every channel (apply_filter_range over [0, N), fused max|y|),
-then the device-side normalize decision/rescale (a no-op unless the peak
-exceeds 1 or --normalize).  N GPUs = N ranks, one file each (weak scaling, no
-data-path collective; --normalize with --peak-scope global adds the RCCL MAX
-all-reduce of the per-file peaks).
+One step = the per-file compute of ProcessFile.cp:57-101 for every file the
+rank owns, through the batch driver (audio-fir-filter_amd/batch.py): filter
+every channel (fused max|y| into the file's peak slot), exchange peaks only if
+a file is split across ranks (or --peak-scope global), then the device-side
+normalize decision and rescale (a no-op unless the peak exceeds 1 or
+--normalize).
 
-Prints ONE JSON line on rank 0 (contract: see README/DESIGN.md).
+  --config 2  (default) one 10-min file per GPU: weak scaling, no collective
+  --config 4  8 x 60-min files over the ranks (one per GPU at N = 8)
+  --config 5  config 4 + --normalize (per-file peaks; --peak-scope global adds
+              the RCCL MAX all-reduce of the north-star variant)
+
+Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
@@ -27,6 +33,7 @@ sys.path.insert(0, os.path.join(ROOT, "audio-fir-filter_amd"))
 
 HBM_PEAK_GBPS = 8000.0      # MI355X_MICROARCH.md:36 (spec)
 FP64_PEAK_TFLOPS = 78.6     # FP64 vector (spec; half the 157.3 TF FP32 vector rate)
+METRIC = "filtered Msamples/sec @4001 taps; achieved HBM GB/s vs roofline"
 
 
 def parse():
@@ -34,8 +41,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", type=int, default=2, choices=[2, 4, 5])
     ap.add_argument("--method", default="auto", choices=["auto", "direct", "fft"])
-    ap.add_argument("--seconds", type=float, default=600.0, help="file length (config 2: 600)")
+    ap.add_argument("--files", type=int, default=None, help="files in the batch (configs 4/5)")
+    ap.add_argument("--seconds", type=float, default=None, help="file length in seconds")
     ap.add_argument("--channels", type=int, default=2)
     ap.add_argument("--fs", type=float, default=48000.0)
     ap.add_argument("--ntaps", type=int, default=4001)
@@ -43,15 +52,22 @@ def parse():
     ap.add_argument("--normalize", action="store_true")
     ap.add_argument("--peak-scope", default="file", choices=["file", "global"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.config == 2:
+        a.seconds = 600.0 if a.seconds is None else a.seconds
+    else:
+        a.files = 8 if a.files is None else a.files
+        a.seconds = 3600.0 if a.seconds is None else a.seconds
+        a.normalize = a.normalize or a.config == 5
+    return a
 
 
 def design_taps(ntaps, fs):
-    """Low-cut taps for the bench (dspguide Blackman windowed-sinc, spectral
-    inversion).  Computed here in numpy so the product path never touches the
-    oracle; the oracle's identical design is used only by the checks."""
+    """Low-cut taps (dspguide Blackman windowed-sinc + spectral inversion),
+    computed here in numpy so the product path never touches the oracle."""
     import numpy as np
     M = ntaps - 1
     half = M // 2
@@ -60,7 +76,7 @@ def design_taps(ntaps, fs):
     d = i - half
     with np.errstate(invalid="ignore", divide="ignore"):
         h = np.where(d == 0, 2 * np.pi * fc, np.sin(2 * np.pi * fc * d) / np.where(d == 0, 1, d))
-    w = 0.42 - 0.5 * np.cos(2 * np.pi * i / M) + 0.08 * np.cos(4 * np.pi * i / M)
+    w = 0.42 - 0.5 * np.cos(2 * np.pi * i / M) + 0.08 * np.cos(4 * np.pi * i / M) if M else 1.0
     h = h * w
     h = -(h / h.sum())
     h[half] += 1.0
@@ -70,7 +86,6 @@ def design_taps(ntaps, fs):
 def cpu_baseline(x0, taps, budget_s):
     """Oracle restatement of the reference threaded CPU path (FilterCore.h +
     ProcessFile.cp:57-87, strict-order double FMA), on a bounded prefix."""
-    import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     try:
@@ -88,13 +103,12 @@ def cpu_baseline(x0, taps, budget_s):
     dt = time.perf_counter() - t
     return {"value": round(n / dt / 1e6, 4), "unit": "Msamples/s", "cores": cores,
             "kind": "port",
-            "sample": f"first {n} samples of channel 0 of the bench file, {taps.size} taps, "
-                      f"oracle ORACLE_FMA three-loop restatement, {cores} pthreads, "
-                      f"{dt:.1f} s"}
+            "sample": f"first {n} samples of channel 0 of file 0, {taps.size} taps, oracle "
+                      f"ORACLE_FMA three-loop restatement, {cores} pthreads, {dt:.1f} s"}
 
 
 def parity_probe(x, y, taps, k=512):
-    """RMS vs the long-double oracle at k sampled positions per channel (rank 0)."""
+    """RMS vs the long-double oracle at sampled positions (rank 0, pre-normalize)."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
@@ -105,11 +119,35 @@ def parity_probe(x, y, taps, k=512):
         n = x.shape[1]
         idx = np.unique(np.r_[np.arange(0, 64), np.arange(n - 64, n), rng.integers(0, n, k),
                               np.arange(half - 8, half + 8)])
+        idx = idx[(idx >= 0) & (idx < n)]
         ref, _ = oracle.filter_points(x[c], taps, idx, oracle.MODE_LD)
         d = y[c][idx].astype(np.float64) - ref
         sq += float((d * d).sum())
         cnt += idx.size
     return (sq / cnt) ** 0.5, cnt
+
+
+class TimedBackend:
+    """batch.DeviceBackend with each filter launch bracketed by HIP events
+    recorded on the launch stream (the dominant kernel's live duration)."""
+
+    def __init__(self, inner, torch):
+        self.inner, self.torch = inner, torch
+        self.events = []
+        self.record = False
+
+    def __getattr__(self, name):
+        return getattr(self.inner, name)
+
+    def filter(self, *a, **k):
+        if not self.record:
+            return self.inner.filter(*a, **k)
+        e0 = self.torch.cuda.Event(enable_timing=True)
+        e1 = self.torch.cuda.Event(enable_timing=True)
+        e0.record(self.inner.stream)
+        self.inner.filter(*a, **k)
+        e1.record(self.inner.stream)
+        self.events.append((e0, e1))
 
 
 def main():
@@ -129,6 +167,7 @@ def main():
 
     import lcfir   # after torch: shares torch's HIP runtime (same SONAME)
     import synth
+    import batch
     lcfir.load()
     runtimes = lcfir.hip_runtimes()
     if len(runtimes) != 1:
@@ -136,100 +175,103 @@ def main():
 
     nch, fs = args.channels, args.fs
     n = int(round(args.seconds * fs))
+    nfiles = world if args.config == 2 else args.files
     taps = design_taps(args.ntaps, fs)
+    half = (args.ntaps - 1) // 2
     bits = args.bits or None
-    # one file per rank: seed offset by the rank (file index)
-    x_host = synth.file_buffer(nch, n, fs, file=rank, bits=bits)
-    x = torch.from_numpy(x_host).to(dev)
-    y = torch.empty_like(x)
-    # per-(file, channel) peak slots: file r owns [r*nch, (r+1)*nch); the file's
-    # peak is the max over its channels (ProcessFile.cp:92-96)
-    peaks = torch.zeros(world * nch, dtype=torch.float32, device=dev)
     flt = lcfir.Filter(taps, device=local, method=args.method)
     method = flt.method
-    stream = torch.cuda.current_stream(dev)
-    sp = stream.cuda_stream
-    my_peaks = peaks[rank * nch:(rank + 1) * nch]
 
-    def step_full(ev=None):
-        lcfir.peak_reset_dev(peaks, peaks.numel(), sp)
-        if ev is not None:
-            ev[0].record(stream)
-        flt.filter_channels_dev(x, n, nch, n, y, n, my_peaks, sp)
-        if ev is not None:
-            ev[1].record(stream)
-        if args.normalize and args.peak_scope == "global" and world > 1:
-            # batch-global peak (north-star config 5 variant; a deviation from the
-            # reference's per-file rule): RCCL MAX all-reduce over xGMI
-            dist.all_reduce(peaks, op=dist.ReduceOp.MAX)
-            lcfir.normalize_dev(y, n, nch, n, peaks, peaks.numel(), True, sp)
-        else:
-            lcfir.normalize_dev(y, n, nch, n, my_peaks, nch, args.normalize, sp)
+    backend = TimedBackend(batch.DeviceBackend(flt, dev), torch)
+    runner = batch.BatchRunner(backend, rank, world, [n] * nfiles, nch, half, args.normalize,
+                               args.peak_scope, batch.torch_allreduce_max())
+    # synthetic samples; configs 4/5 reuse two generated files to bound host time
+    cache = {}
+
+    def file_samples(f):
+        key = f if args.config == 2 else f % 2
+        if key not in cache:
+            cache[key] = synth.file_buffer(nch, n, fs, file=key, bits=bits)
+        return cache[key]
+
+    runner.prepare(lambda f, lo, hi: file_samples(f)[:, lo:hi])
+    my_samples = sum(nch * (sh.end - sh.start) for sh in runner.shards)
 
     for _ in range(args.warmup):
-        step_full()
+        runner.step()
     torch.cuda.synchronize(dev)
-
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    backend.record = True
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        step_full(evs[i])
+    for _ in range(args.steps):
+        runner.step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / max(1, args.steps)
+    backend.record = False
+    launches = len(backend.events)
+    kern_ms = sum(a.elapsed_time(b) for a, b in backend.events) / max(1, launches)
+    samples_per_launch = my_samples / max(1, len(runner.shards))
 
+    total_samples = torch.tensor([float(my_samples)], dtype=torch.float64, device=dev)
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
-
-    samples_per_step = nch * n
-    total = samples_per_step * args.steps * world
+        dist.all_reduce(total_samples, op=dist.ReduceOp.SUM)
+    total = float(total_samples[0]) * args.steps
     value = total / elapsed / 1e6
-    ms_per_step = elapsed / args.steps * 1e3
     kern_s = kern_ms / 1e3
-    achieved = 4.0 * samples_per_step / kern_s / 1e9
-    fp64_tflops = 2.0 * args.ntaps * samples_per_step / kern_s / 1e12
+    achieved = 4.0 * samples_per_launch / kern_s / 1e9
+    direct_tflops = 2.0 * args.ntaps * samples_per_launch / kern_s / 1e12
 
     if rank == 0:
-        y_host = y.cpu().numpy()
-        rms, npos = parity_probe(x_host, y_host, taps)
+        rms, npos = None, 0
+        if not args.no_parity and runner.shards:
+            # parity of this rank's first file, recomputed without the normalize pass
+            x = np.ascontiguousarray(file_samples(runner.shards[0].file))
+            xd = torch.from_numpy(x).to(dev)
+            y = torch.empty_like(xd)
+            flt.filter_channels_dev(xd, n, nch, n, y, n, None, torch.cuda.current_stream(dev).cuda_stream)
+            torch.cuda.synchronize(dev)
+            rms, npos = parity_probe(x, y.cpu().numpy(), taps)
+            del xd, y
         traffic = None
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
             if tj.get("method") == method and tj.get("ntaps") == args.ntaps and \
-                    tj.get("samples_per_launch") == samples_per_step:
+                    tj.get("samples_per_launch") == samples_per_launch:
                 traffic = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             pass
+        wl = {2: "config2: 10 min stereo 48 kHz int24 file per GPU",
+              4: f"config4: {nfiles} x {args.seconds / 60:g} min stereo 48 kHz int24 files",
+              5: f"config5: {nfiles} x {args.seconds / 60:g} min stereo 48 kHz int24 files, "
+                 f"--normalize"}
         line = {
-            "metric": "filtered Msamples/sec @4001 taps; achieved HBM GB/s vs roofline",
+            "metric": METRIC,
             "value": round(value, 3),
             "unit": "Msamples/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4),
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if args.config == 2 else "strong",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (SURVEY.md s8d int24 generator), resident in HBM",
             "config": {
-                "workload": f"config2: {args.seconds / 60:g} min {nch}-ch {fs / 1000:g} kHz "
-                            f"{'int%d' % bits if bits else 'float32'} file per GPU, "
-                            f"{args.ntaps}-tap low-cut",
-                "channels": nch, "samples_per_channel": n, "ntaps": args.ntaps,
-                "method": method, "files_per_gpu": 1,
-                "parallelism": f"one file per GPU x{world}",
+                "workload": wl[args.config] + f", {args.ntaps}-tap low-cut",
+                "files": nfiles, "channels": nch, "samples_per_channel": n,
+                "ntaps": args.ntaps, "method": method,
+                "parallelism": f"{world} rank(s), files sharded by batch.plan_shards",
                 "normalize": bool(args.normalize), "peak_scope": args.peak_scope,
+                "peak_exchange": runner.exchange,
             },
             "roofline": {
                 "bound": "hbm",
@@ -240,15 +282,17 @@ def main():
                 "traffic": traffic,
                 "kernel": "fir_direct_f64_kernel" if method == "direct" else "fir_fft_f64_kernel",
                 "kernel_ms": round(kern_ms, 4),
+                "launches_timed": launches,
                 "bytes_per_unit": 4,
                 "binding": "fp64-valu",
-                "fp64_tflops": round(fp64_tflops, 3),
-                "fp64_frac": round(fp64_tflops / FP64_PEAK_TFLOPS, 4),
+                "direct_equiv_fp64_tflops": round(direct_tflops, 3),
+                "fp64_frac": round(direct_tflops / FP64_PEAK_TFLOPS, 4) if method == "direct"
+                else None,
             },
             "parity": {"rms_vs_longdouble": rms, "positions": npos, "tol": 1e-9},
         }
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(x_host[0], taps, args.cpu_seconds)
+            line["cpu_baseline"] = cpu_baseline(file_samples(0)[0], taps, args.cpu_seconds)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

@@ -100,6 +100,19 @@ int lcfir_filter_channels_dev(lcfir_ctx *ctx, const float *d_x, int64_t x_stride
                               int64_t n, float *d_y, int64_t y_stride, float *d_peak,
                               void *stream);
 
+/* General windowed form, for a file sharded across processes/GPUs by sample
+ * range: the caller holds only samples [x_lo, x_hi) of channels that are n
+ * samples long (channel c's window at d_xw + c*x_stride, element 0 = sample
+ * x_lo) and wants outputs [start, end) (channel c's at d_yw + c*y_stride,
+ * element 0 = output y_lo).  The window must cover
+ * [max(0, start - half), min(n, end + half)).  d_peak (nullable): channel c's
+ * max|y| is max-ed into d_peak[c * peak_stride] (peak_stride 0 folds every
+ * channel into one per-file slot, ProcessFile.cp:92-96). */
+int lcfir_filter_window_dev(lcfir_ctx *ctx, const float *d_xw, int64_t x_lo, int64_t x_hi,
+                            int64_t x_stride, int64_t n, int32_t nch, float *d_yw, int64_t y_lo,
+                            int64_t y_stride, int64_t start, int64_t end, float *d_peak,
+                            int64_t peak_stride, void *stream);
+
 /* ---- peak + normalize post-pass (ProcessFile.cp:91-101) ----------------- */
 /* max_mag() over each channel (VectorMath::max_mag); d_peak[c] = max(d_peak[c], max|y_c|). */
 int lcfir_peak_reset_dev(float *d_peak, int32_t count, void *stream);

@@ -1,0 +1,165 @@
+"""Multi-process (gloo, CPU) tests of the batch driver's sharding and peak
+exchange.  The compute is the oracle (tests only), so these
+check the host logic: shard plans, windows, the MAX all-reduce of the
+per-file peak vector and the per-file / batch-global normalize rule, against
+a single-process run of the reference path (ProcessFile.cp:57-101)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import batch
+
+HALF = 100  # 201 taps
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def make_files(nfiles, nch, n, loud):
+    import synth
+    files = []
+    for f in range(nfiles):
+        x = synth.file_buffer(nch, n + 37 * f, 48000.0, file=f, bits=24)
+        if loud and f % 2 == 0:
+            x = (x * np.float32(3.0)).astype(np.float32)  # peak > 1 after filtering
+        files.append(np.ascontiguousarray(x))
+    return files
+
+
+def make_taps():
+    import oracle
+    return oracle.design_lowcut(300.0, 48000.0, 2 * HALF + 1)
+
+
+class OracleBackend(batch.Backend):
+    """CPU stand-in for DeviceBackend built on the oracle (tests only)."""
+
+    def __init__(self, taps):
+        import oracle
+        self.o, self.taps = oracle, taps
+
+    def new_peaks(self, nfiles):
+        return np.zeros(max(1, nfiles), np.float32)
+
+    def upload(self, file, xw, x_lo, x_hi):
+        return np.ascontiguousarray(xw, np.float32)
+
+    def alloc_out(self, nch, count):
+        return np.zeros((nch, count), np.float32)
+
+    def zero_peaks(self, peaks):
+        peaks[:] = 0
+
+    def filter(self, xw, x_lo, x_hi, n, nch, yw, start, end, peaks, slot):
+        for c in range(nch):
+            xf = np.zeros(n, np.float32)
+            xf[x_lo:x_hi] = xw[c]
+            y = np.zeros(n, np.float32)
+            self.o.apply_filter_range(xf, self.taps, y, start, end, self.o.MODE_FMA)
+            yw[c] = y[start:end]
+        peaks[slot] = max(peaks[slot], np.abs(yw).max() if yw.size else 0.0)
+
+    def normalize(self, yw, nch, count, peaks, slot, force):
+        p = float(peaks.max() if slot is None else peaks[slot])
+        if (p > 1.0 or force) and p > 0.0:
+            yw[:] = (yw.astype(np.float64) * (1.0 / p)).astype(np.float32)
+
+
+def _worker(rank, world, port, nfiles, nch, n, normalize, scope, loud, q):
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    try:
+        files = make_files(nfiles, nch, n, loud)
+        taps = make_taps()
+
+        def allreduce(peaks):
+            t = torch.from_numpy(peaks)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+
+        r = batch.BatchRunner(OracleBackend(taps), rank, world, [f.shape[1] for f in files], nch,
+                              HALF, normalize, scope, allreduce)
+        r.prepare(lambda f, lo, hi: files[f][:, lo:hi])
+        r.step()
+        q.put((rank, r.exchange, [(sh, y.copy()) for sh, y in r.results()]))
+    finally:
+        dist.destroy_process_group()
+
+
+def run_dist(world, nfiles, nch, n, normalize, scope, loud):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, nfiles, nch, n, normalize, scope,
+                                                loud, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return got
+
+
+def reference(nfiles, nch, n, normalize, scope, loud):
+    import oracle
+    files = make_files(nfiles, nch, n, loud)
+    taps = make_taps()
+    if scope == "file":
+        out = []
+        for x in files:
+            buf = x.copy()
+            oracle.process_buffer(buf, taps, nthreads=1, normalize=normalize, mode=oracle.MODE_FMA)
+            out.append(buf)
+        return out
+    ys = [np.stack([oracle.filter_channel(x[c], taps, oracle.MODE_FMA) for c in range(nch)])
+          for x in files]
+    peak = max(float(np.abs(y).max()) for y in ys)
+    if (peak > 1.0 or normalize) and peak > 0:
+        ys = [(y.astype(np.float64) * (1.0 / peak)).astype(np.float32) for y in ys]
+    return ys
+
+
+@pytest.mark.parametrize("world,nfiles,normalize,scope,loud,exchange", [
+    (2, 2, False, "file", True, False),   # one file per rank: no collective
+    (2, 2, True, "file", False, False),
+    (2, 3, False, "file", True, False),   # 3 files over 2 ranks
+    (2, 1, False, "file", True, True),    # one file split over 2 ranks: peak exchange
+    (2, 1, True, "file", False, True),
+    (3, 2, True, "file", True, True),     # 2 files over 3 ranks (one split)
+    (2, 2, True, "global", False, True),  # batch-global variant
+])
+def test_batch_matches_serial_reference(world, nfiles, normalize, scope, loud, exchange):
+    nch, n = 2, 3000
+    got = run_dist(world, nfiles, nch, n, normalize, scope, loud)
+    ref = reference(nfiles, nch, n, normalize, scope, loud)
+    assembled = [np.full_like(r, np.nan) for r in ref]
+    for rank, ex, shards in got:
+        assert ex == exchange
+        for sh, y in shards:
+            assembled[sh.file][:, sh.start:sh.end] = y
+    for a, r in zip(assembled, ref):
+        assert np.array_equal(a, r)
+
+
+def test_plan_shards_rules():
+    p = batch.plan_shards([100, 200, 300, 400, 500, 600, 700, 800], 8)
+    assert all(len(s) == 1 and s[0].start == 0 for s in p)  # one file per GPU
+    assert not batch.file_is_split(p)
+    p = batch.plan_shards([1000], 4)
+    assert [(s[0].start, s[0].end) for s in p] == [(0, 250), (250, 500), (500, 750), (750, 1000)]
+    assert batch.file_is_split(p)
+    p = batch.plan_shards([10, 11, 12], 2)
+    assert [[sh.file for sh in s] for s in p] == [[0, 2], [1]]
+    p = batch.plan_shards([1001, 10], 3)  # file 0 over ranks 0-1, file 1 on rank 2
+    assert [(s[0].file, s[0].start, s[0].end) for s in p] == [(0, 0, 500), (0, 500, 1001), (1, 0, 10)]
+    assert batch.window(batch.Shard(0, 500, 1001), 1001, 100) == (400, 1001)

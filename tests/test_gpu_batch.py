@@ -1,0 +1,88 @@
+"""GPU tests of the sharded-file entry point (lcfir_filter_window_dev) and of
+the batch driver's DeviceBackend (single rank), against the oracle."""
+import numpy as np
+import pytest
+
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+RMS_TOL = 1e-9
+
+
+@pytest.fixture(scope="module")
+def tt():
+    import torch  # before lcfir: one HIP runtime in the process
+    assert torch.cuda.is_available()
+    import lcfir
+    lcfir.load()
+    assert len(lcfir.hip_runtimes()) == 1, lcfir.hip_runtimes()
+    return torch, lcfir
+
+
+def rms(a, b):
+    d = np.asarray(a, np.float64) - np.asarray(b, np.float64)
+    return float(np.sqrt(np.mean(d * d))) if d.size else 0.0
+
+
+@pytest.mark.parametrize("method", ["direct", "fft"])
+def test_filter_window_matches_oracle(tt, oracle_mod, method):
+    torch, lc = tt
+    g = load_golden("float_source")
+    x, taps = g["x"][:3], g["taps"]        # 3 channels x 3000, 1601 taps
+    nch, n = x.shape
+    half = (taps.size - 1) // 2
+    flt = lc.Filter(taps, method=method)
+    ref = np.stack([oracle_mod.filter_channel(x[c], taps, oracle_mod.MODE_FMA) for c in range(nch)])
+    # odd and even window edges, ranges touching both ends, a 1-sample range
+    for start, end in [(0, n), (1, 2999), (777, 1501), (2998, 2999), (0, 5), (1333, 3000)]:
+        lo, hi = max(0, start - half), min(n, end + half)
+        for extra_lo, extra_hi in [(0, 0), (min(lo, 3), min(n - hi, 5))]:
+            wlo, whi = lo - extra_lo, hi + extra_hi
+            xw = torch.from_numpy(np.ascontiguousarray(x[:, wlo:whi])).cuda()
+            yw = torch.full((nch, end - start), 7.0, dtype=torch.float32, device="cuda")
+            pk = torch.zeros(1, dtype=torch.float32, device="cuda")
+            flt.filter_window_dev(xw, wlo, whi, whi - wlo, n, nch, yw, start, end - start, start,
+                                  end, pk, 0, peak_stride=0)
+            torch.cuda.synchronize()
+            y = yw.cpu().numpy()
+            if method == "direct":
+                assert np.array_equal(y, ref[:, start:end]), (start, end)
+            for c in range(nch):
+                assert rms(y[c], g["y"][c][start:end]) <= RMS_TOL
+            assert pk.item() == np.abs(y).max()
+
+
+def test_filter_window_rejects_short_window(tt):
+    torch, lc = tt
+    flt = lc.Filter(np.ones(101))
+    xw = torch.zeros((1, 100), device="cuda")
+    yw = torch.zeros((1, 10), device="cuda")
+    with pytest.raises(lc.LcfirError) as e:
+        flt.filter_window_dev(xw, 500, 600, 100, 1000, 1, yw, 540, 10, 540, 550)
+    assert "does not cover" in str(e.value)
+
+
+@pytest.mark.parametrize("normalize,loud", [(False, False), (True, False), (False, True)])
+def test_device_batch_runner(tt, oracle_mod, normalize, loud):
+    """One rank, three files: BatchRunner + DeviceBackend vs ProcessFile.cp:57-101."""
+    torch, lc = tt
+    import batch
+    import synth
+    taps = oracle_mod.design_lowcut(20.0, 48000.0, 801)
+    files = [synth.file_buffer(2, 20000 + 1001 * f, 48000.0, file=f, bits=24) for f in range(3)]
+    if loud:
+        files[1] = (files[1] * np.float32(3.0)).astype(np.float32)
+    flt = lc.Filter(taps, method="direct")
+    r = batch.BatchRunner(batch.DeviceBackend(flt, torch.device("cuda", 0)), 0, 1,
+                          [f.shape[1] for f in files], 2, 400, normalize, "file")
+    r.prepare(lambda f, lo, hi: files[f][:, lo:hi])
+    r.step()
+    r.step()  # steps are repeatable (peaks reset each step)
+    torch.cuda.synchronize()
+    assert not r.exchange
+    for sh, y in r.results():
+        ref = files[sh.file].copy()
+        oracle_mod.process_buffer(ref, taps, nthreads=1, normalize=normalize,
+                                  mode=oracle_mod.MODE_FMA)
+        assert np.array_equal(y.cpu().numpy(), ref[:, sh.start:sh.end])
