@@ -103,8 +103,9 @@ def cpu_baseline(x0, taps, budget_s):
     dt = time.perf_counter() - t
     return {"value": round(n / dt / 1e6, 4), "unit": "Msamples/s", "cores": cores,
             "kind": "port",
-            "sample": f"first {n} samples of channel 0 of file 0, {taps.size} taps, oracle "
-                      f"ORACLE_FMA three-loop restatement, {cores} pthreads, {dt:.1f} s"}
+            "sample": f"first {n} samples of file 0 (channels laid end to end), {taps.size} "
+                      f"taps, oracle ORACLE_FMA three-loop restatement, {cores} pthreads, "
+                      f"{dt:.1f} s"}
 
 
 def parity_probe(x, y, taps, k=512):
@@ -292,7 +293,8 @@ def main():
             "parity": {"rms_vs_longdouble": rms, "positions": npos, "tol": 1e-9},
         }
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(file_samples(0)[0], taps, args.cpu_seconds)
+            line["cpu_baseline"] = cpu_baseline(file_samples(0).reshape(-1), taps,
+                                                args.cpu_seconds)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

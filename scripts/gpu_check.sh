@@ -1,10 +1,12 @@
 #!/bin/bash
-# GPU-box check: smoke -> pytest -m gpu -> bench -> rocprofv3 kernel stats.
+# GPU-box check: smoke -> pytest -m gpu -> bench -> rocprofv3 kernel stats ->
+# PMC HBM traffic (FETCH_SIZE / WRITE_SIZE, separate passes) -> traffic json.
 # Every GPU step has its own time limit; the first failure ends the script.
-# usage (from the repo root, on the GPU box): bash scripts/gpu_check.sh [bench args...]
+# usage (from the repo root, on the GPU box): bash scripts/gpu_check.sh [tag] [bench args...]
 set -u -o pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$ROOT"
+TAG=${1:-run}; shift || true
 OUT="$ROOT/gpurun_out"
 mkdir -p "$OUT"
 step() { # name timeout cmd...
@@ -12,14 +14,21 @@ step() { # name timeout cmd...
     echo "== $name ($(date +%T))"
     timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
     local rc=$?
-    tail -5 "$OUT/$name.log"
+    tail -3 "$OUT/$name.log" | cut -c1-3000
     if [ $rc -ne 0 ]; then echo "!! $name failed rc=$rc"; tail -40 "$OUT/$name.log"; exit $rc; fi
 }
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step pytest_gpu 1200 python -m pytest tests -m gpu -x -q
-step bench 600 python bench.py --steps 10 --warmup 2 "$@"
+step bench 600 python bench.py --steps 20 --warmup 3 "$@"
 cd /tmp && export TMPDIR=/tmp
-step rocprof 600 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof" -o bench -- \
-    python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline "$@"
-find "$OUT/prof" -name "*kernel_stats*" -exec cp {} "$OUT/" \;
+step rocprof 600 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof_$TAG" -o bench -- \
+    python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --no-parity "$@"
+cp "$OUT/prof_$TAG/bench_kernel_stats.csv" "$OUT/kernel_stats_$TAG.csv"
+for c in FETCH_SIZE WRITE_SIZE; do
+    step "pmc_$c" 600 rocprofv3 --pmc $c --kernel-include-regex 'fir_' -f csv \
+        -d "$OUT/pmc_$TAG/p_$c" -o pmc -- \
+        python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-parity "$@"
+done
+cd "$ROOT"
+python scripts/pmc_summary.py "$OUT/pmc_$TAG" --json "$OUT/pmc_summary_$TAG.json" > /dev/null
 echo "== done"

@@ -1,0 +1,43 @@
+"""Turn a PMC summary (scripts/pmc_summary.py output) into profiles/traffic_latest.json,
+the per-launch HBM traffic bench.py reports as roofline.traffic.
+
+usage: python scripts/make_traffic_json.py <pmc_summary.json> <out.json> --method fft \
+           --ntaps 4001 --samples-per-launch 57600000 --kernel fir_fft_f64_kernel
+
+HBM bytes per launch = 2 * FETCH_SIZE * 1024 (gfx950 FETCH_SIZE counts half the
+bytes of wide streaming reads: MI355X_MICROARCH.md, HBM section) + WRITE_SIZE * 1024.
+"""
+import argparse
+import json
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("summary")
+    ap.add_argument("out")
+    ap.add_argument("--method", required=True)
+    ap.add_argument("--ntaps", type=int, required=True)
+    ap.add_argument("--samples-per-launch", type=float, required=True)
+    ap.add_argument("--kernel", required=True)
+    a = ap.parse_args()
+    s = json.load(open(a.summary))
+    k = next(v for name, v in s.items() if a.kernel in name)
+    read = 2.0 * k["FETCH_SIZE"] * 1024.0
+    write = k["WRITE_SIZE"] * 1024.0
+    alg = 8.0 * a.samples_per_launch
+    out = {
+        "method": a.method, "ntaps": a.ntaps, "samples_per_launch": a.samples_per_launch,
+        "kernel": a.kernel,
+        "hbm_bytes_per_launch": read + write,
+        "hbm_read_bytes_per_launch": read, "hbm_write_bytes_per_launch": write,
+        "algorithmic_rw_bytes_per_launch": alg,
+        "traffic_over_algorithmic": (read + write) / alg,
+        "avg_duration_ns_profiled": k.get("avg_duration_ns"),
+        "note": "FETCH_SIZE doubled per the gfx950 calibration; separate rocprofv3 --pmc passes",
+    }
+    json.dump(out, open(a.out, "w"), indent=1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
