@@ -24,6 +24,7 @@
 #include <string>
 #include <vector>
 
+#include "codec.hpp"
 #include "fir_direct.hpp"
 #include "fir_fft.hpp"
 #include "peak_scale.hpp"
@@ -468,6 +469,58 @@ int lcfir_channel_peak(int device, const float *y, int64_t n, float *peak) {
         rc = fail(LCFIR_EDEVICE, "peak kernel failed");
     return_staging(st);
     return rc;
+}
+
+static bool pcm_format(int format, lcfir::PcmFormat &f) {
+    switch (format) {
+    case LCFIR_PCM_S16LE: f = {2, false, false}; return true;
+    case LCFIR_PCM_S24LE: f = {3, false, false}; return true;
+    case LCFIR_PCM_S32LE: f = {4, false, false}; return true;
+    case LCFIR_PCM_F32LE: f = {4, true, false}; return true;
+    case LCFIR_PCM_S16BE: f = {2, false, true}; return true;
+    case LCFIR_PCM_S24BE: f = {3, false, true}; return true;
+    case LCFIR_PCM_S32BE: f = {4, false, true}; return true;
+    case LCFIR_PCM_F32BE: f = {4, true, true}; return true;
+    default: return false;
+    }
+}
+
+int lcfir_pcm_bytes(int format) {
+    lcfir::PcmFormat f;
+    return pcm_format(format, f) ? f.bytes : 0;
+}
+
+int lcfir_decode_pcm_dev(const void *d_in, int format, int32_t nch, int64_t frames,
+                         float *d_out, int64_t out_stride, void *stream) {
+    lcfir::PcmFormat f;
+    if (!pcm_format(format, f)) return fail(LCFIR_EINVAL, "unknown PCM format %d", format);
+    if (nch < 0 || frames < 0) return fail(LCFIR_EINVAL, "negative size");
+    if (nch == 0 || frames == 0) return LCFIR_OK;
+    if (!d_in || !d_out) return fail(LCFIR_EINVAL, "null argument");
+    if (nch > 1 && out_stride < frames) return fail(LCFIR_EINVAL, "channel stride < frames");
+    const int blocks = stream_blocks(frames * nch, 256 * 8);
+    hipLaunchKernelGGL(lcfir::decode_pcm_kernel, dim3(blocks), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream),
+                       reinterpret_cast<const uint8_t *>(d_in), f, (int)nch, frames, d_out,
+                       out_stride);
+    LCFIR_HIP(hipGetLastError());
+    return LCFIR_OK;
+}
+
+int lcfir_encode_pcm_dev(const float *d_in, int64_t in_stride, int32_t nch, int64_t frames,
+                         int format, void *d_out, void *stream) {
+    lcfir::PcmFormat f;
+    if (!pcm_format(format, f)) return fail(LCFIR_EINVAL, "unknown PCM format %d", format);
+    if (nch < 0 || frames < 0) return fail(LCFIR_EINVAL, "negative size");
+    if (nch == 0 || frames == 0) return LCFIR_OK;
+    if (!d_in || !d_out) return fail(LCFIR_EINVAL, "null argument");
+    if (nch > 1 && in_stride < frames) return fail(LCFIR_EINVAL, "channel stride < frames");
+    const int blocks = stream_blocks(frames * nch, 256 * 8);
+    hipLaunchKernelGGL(lcfir::encode_pcm_kernel, dim3(blocks), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), d_in, in_stride, (int)nch, frames,
+                       f, reinterpret_cast<uint8_t *>(d_out));
+    LCFIR_HIP(hipGetLastError());
+    return LCFIR_OK;
 }
 
 int lcfir_dev_malloc(int device, size_t bytes, void **out) {

@@ -65,6 +65,9 @@ _SIGNATURES = {
     "lcfir_peak_dev": ([_vp, _c_i64, _c_i32, _c_i64, _vp, _vp], _c_int),
     "lcfir_normalize_dev": ([_vp, _c_i64, _c_i32, _c_i64, _vp, _c_i32, _c_int, _vp], _c_int),
     "lcfir_channel_peak": ([_c_int, _vp, _c_i64, ctypes.POINTER(ctypes.c_float)], _c_int),
+    "lcfir_pcm_bytes": ([_c_int], _c_int),
+    "lcfir_decode_pcm_dev": ([_vp, _c_int, _c_i32, _c_i64, _vp, _c_i64, _vp], _c_int),
+    "lcfir_encode_pcm_dev": ([_vp, _c_i64, _c_i32, _c_i64, _c_int, _vp, _vp], _c_int),
     "lcfir_dev_malloc": ([_c_int, ctypes.c_size_t, ctypes.POINTER(_vp)], _c_int),
     "lcfir_dev_free": ([_vp], _c_int),
     "lcfir_memcpy_h2d": ([_vp, _vp, ctypes.c_size_t, _vp], _c_int),
@@ -366,3 +369,24 @@ def hip_runtimes() -> list:
     except OSError:
         pass
     return sorted(paths)
+
+
+# -- sample codec (interleaved PCM <-> planar float32) --------------------------
+PCM_FORMATS = {"s16le": 1, "s24le": 2, "s32le": 3, "f32le": 4,
+               "s16be": 5, "s24be": 6, "s32be": 7, "f32be": 8}
+
+
+def pcm_bytes(fmt: str) -> int:
+    return load().lcfir_pcm_bytes(PCM_FORMATS[fmt])
+
+
+def decode_pcm_dev(d_in, fmt: str, nch: int, frames: int, d_out, out_stride: int, stream=0):
+    """Interleaved PCM bytes (device) -> planar float32 [nch][out_stride] (device)."""
+    _check(load().lcfir_decode_pcm_dev(_ptr(d_in), PCM_FORMATS[fmt], nch, frames, _ptr(d_out),
+                                       out_stride, stream or None))
+
+
+def encode_pcm_dev(d_in, in_stride: int, nch: int, frames: int, fmt: str, d_out, stream=0):
+    """Planar float32 (device) -> interleaved PCM bytes (device)."""
+    _check(load().lcfir_encode_pcm_dev(_ptr(d_in), in_stride, nch, frames, PCM_FORMATS[fmt],
+                                       _ptr(d_out), stream or None))

@@ -127,6 +127,31 @@ int lcfir_normalize_dev(float *d_y, int64_t stride, int32_t nch, int64_t n,
 /* Host-pointer convenience: max|y| of one channel (VectorMath::max_mag). */
 int lcfir_channel_peak(int device, const float *y, int64_t n, float *peak);
 
+/* ---- sample codec either side of the path -------- */
+/* Interleaved PCM frames (WAV little-endian / AIFF big-endian) <-> the
+ * deinterleaved float32 AudioBuffer the hot path works on.  Replaces, on the
+ * device, c_lib's AudioSamples::readAll (ProcessFile.cp:40-41) and
+ * AudioSamples::writeAll(buf, true) (:115-117), whose exact conventions are
+ * unpinned; ours: int b-bit v <-> v / 2^(b-1), encode rounds half-to-even in
+ * f64 and clamps to [-2^(b-1), 2^(b-1) - 1]; float32 is passed through. */
+typedef enum lcfir_pcm_format {
+    LCFIR_PCM_S16LE = 1,
+    LCFIR_PCM_S24LE = 2, /* packed 3-byte */
+    LCFIR_PCM_S32LE = 3,
+    LCFIR_PCM_F32LE = 4,
+    LCFIR_PCM_S16BE = 5,
+    LCFIR_PCM_S24BE = 6,
+    LCFIR_PCM_S32BE = 7,
+    LCFIR_PCM_F32BE = 8
+} lcfir_pcm_format;
+
+int lcfir_pcm_bytes(int format); /* bytes per sample, 0 for an unknown format */
+/* d_in: frames * nch interleaved samples; channel c goes to d_out + c*out_stride. */
+int lcfir_decode_pcm_dev(const void *d_in, int format, int32_t nch, int64_t frames,
+                         float *d_out, int64_t out_stride, void *stream);
+int lcfir_encode_pcm_dev(const float *d_in, int64_t in_stride, int32_t nch, int64_t frames,
+                         int format, void *d_out, void *stream);
+
 /* ---- device memory / stream helpers for hosts without a GPU runtime ----- */
 int lcfir_dev_malloc(int device, size_t bytes, void **out);
 int lcfir_dev_free(void *p);
