@@ -471,6 +471,38 @@ int lcfir_channel_peak(int device, const float *y, int64_t n, float *peak) {
     return rc;
 }
 
+int lcfir_design_lowcut(double freq_hz, double slope_hz, double fs, double *taps, int32_t cap,
+                        int32_t *ntaps) {
+    if (!ntaps) return fail(LCFIR_EINVAL, "ntaps is null");
+    if (!(fs > 0.0) || !(slope_hz > 0.0) || !(freq_hz >= 0.0) || !(freq_hz < fs / 2))
+        return fail(LCFIR_EINVAL, "need fs > 0, slope > 0, 0 <= freq < fs/2");
+    const long double bw = (long double)slope_hz / (long double)fs;
+    const long double half_m = 2.0L / bw; // M / 2
+    const long long hm = std::max<long long>(1, llroundl(half_m));
+    if (hm > (1LL << 26)) return fail(LCFIR_EINVAL, "kernel too long (slope too small)");
+    const int32_t T = (int32_t)(2 * hm + 1);
+    *ntaps = T;
+    if (!taps) return LCFIR_OK;
+    if (cap < T) return fail(LCFIR_EINVAL, "cap %d < %d taps", cap, T);
+    const int M = T - 1, half = M / 2;
+    const long double fc = (long double)freq_hz / (long double)fs;
+    const long double two_pi = 6.283185307179586476925286766559L;
+    std::vector<long double> h((size_t)T);
+    long double sum = 0.0L;
+    for (int i = 0; i <= M; ++i) {
+        const int d = i - half;
+        const long double v = d == 0 ? two_pi * fc : sinl(two_pi * fc * (long double)d) / (long double)d;
+        const long double w = 0.42L - 0.5L * cosl(two_pi * (long double)i / (long double)M) +
+                              0.08L * cosl(2.0L * two_pi * (long double)i / (long double)M);
+        h[(size_t)i] = v * w;
+        sum += h[(size_t)i];
+    }
+    for (int i = 0; i <= M; ++i) h[(size_t)i] = -(h[(size_t)i] / sum); // unity DC gain, inverted
+    h[(size_t)half] += 1.0L;                                             // spectral inversion
+    for (int i = 0; i <= M; ++i) taps[i] = (double)h[(size_t)i];
+    return LCFIR_OK;
+}
+
 static bool pcm_format(int format, lcfir::PcmFormat &f) {
     switch (format) {
     case LCFIR_PCM_S16LE: f = {2, false, false}; return true;

@@ -65,6 +65,8 @@ _SIGNATURES = {
     "lcfir_peak_dev": ([_vp, _c_i64, _c_i32, _c_i64, _vp, _vp], _c_int),
     "lcfir_normalize_dev": ([_vp, _c_i64, _c_i32, _c_i64, _vp, _c_i32, _c_int, _vp], _c_int),
     "lcfir_channel_peak": ([_c_int, _vp, _c_i64, ctypes.POINTER(ctypes.c_float)], _c_int),
+    "lcfir_design_lowcut": ([ctypes.c_double, ctypes.c_double, ctypes.c_double, _vp, _c_i32,
+                             ctypes.POINTER(_c_i32)], _c_int),
     "lcfir_pcm_bytes": ([_c_int], _c_int),
     "lcfir_decode_pcm_dev": ([_vp, _c_int, _c_i32, _c_i64, _vp, _c_i64, _vp], _c_int),
     "lcfir_encode_pcm_dev": ([_vp, _c_i64, _c_i32, _c_i64, _c_int, _vp, _vp], _c_int),
@@ -369,6 +371,18 @@ def hip_runtimes() -> list:
     except OSError:
         pass
     return sorted(paths)
+
+
+# -- tap design (ProcessFile.cp:47-50) ------------------------------------------
+def design_lowcut(freq_hz: float, slope_hz: float, fs: float) -> np.ndarray:
+    """Low-cut taps as the reference builds them per file (host, long double)."""
+    lib = load()
+    n = ctypes.c_int32()
+    _check(lib.lcfir_design_lowcut(freq_hz, slope_hz, fs, None, 0, ctypes.byref(n)))
+    taps = np.zeros(n.value, np.float64)
+    _check(lib.lcfir_design_lowcut(freq_hz, slope_hz, fs, taps.ctypes.data, n.value,
+                                   ctypes.byref(n)))
+    return taps
 
 
 # -- sample codec (interleaved PCM <-> planar float32) --------------------------

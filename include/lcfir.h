@@ -127,6 +127,17 @@ int lcfir_normalize_dev(float *d_y, int64_t stride, int32_t nch, int64_t n,
 /* Host-pointer convenience: max|y| of one channel (VectorMath::max_mag). */
 int lcfir_channel_peak(int device, const float *y, int64_t n, float *peak);
 
+/* ---- tap design (host, long double) ---------------- */
+/* Replaces `WindowedSinc<float64_t> sinc(freq / fs, slope / fs); sinc.makeLowCut();`
+ * (ProcessFile.cp:47-50): dspguide ch.16 Blackman windowed-sinc low-pass with
+ * unity DC gain, then spectral inversion to a high-pass (README.md:50,60-62).
+ * Kernel length M + 1 with M = 4 / (slope / fs) rounded to the nearest even
+ * integer (c_lib's exact rounding rule is unpinned).  Writes *ntaps; if taps
+ * is non-NULL and cap >= *ntaps, also writes the taps.  -s 48 at 48 kHz
+ * gives 4001 taps, -s 10 at 48 kHz 19 201. */
+int lcfir_design_lowcut(double freq_hz, double slope_hz, double fs, double *taps, int32_t cap,
+                        int32_t *ntaps);
+
 /* ---- sample codec either side of the path -------- */
 /* Interleaved PCM frames (WAV little-endian / AIFF big-endian) <-> the
  * deinterleaved float32 AudioBuffer the hot path works on.  Replaces, on the

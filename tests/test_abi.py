@@ -68,6 +68,26 @@ def test_python_binding_fails_loudly_without_library(tmp_path):
             lcfir._lib = lcfir._lib_saved
 
 
+@pytest.mark.parametrize("freq,slope,fs", [(20, 48, 48000), (20, 10, 48000), (20, 96, 96000),
+                                           (15, 10, 44100), (440, 80, 48000)])
+def test_design_lowcut_matches_oracle(oracle_mod, freq, slope, fs):
+    """Host tap design (ProcessFile.cp:47-50) vs the oracle's restatement."""
+    taps = lcfir.design_lowcut(freq, slope, fs)
+    assert taps.size == oracle_mod.lowcut_ntaps(slope, fs)
+    ref = oracle_mod.design_lowcut(freq, fs, taps.size)
+    # same long-double formula compiled by two compilers: agreement to a few
+    # ulps of the largest tap (tiny taps near the window's zeros are noise-level)
+    assert np.abs(taps - ref).max() <= 4 * np.spacing(np.abs(ref).max())
+    assert abs(taps.sum()) < 1e-12 and 0.9 < taps[taps.size // 2] < 1.0
+
+
+def test_design_lowcut_rejects_bad_args():
+    with pytest.raises(lcfir.LcfirError):
+        lcfir.design_lowcut(20, 0, 48000)
+    with pytest.raises(lcfir.LcfirError):
+        lcfir.design_lowcut(30000, 10, 48000)
+
+
 def test_header_declares_reference_citations():
     text = open(lcfir.HEADER_PATH).read()
     for cite in ("FilterCore.h:20-27", "FilterCore.h:20-79", "ProcessFile.cp:91-101",
