@@ -587,6 +587,27 @@ int lcfir_memcpy_d2h(void *dst, const void *src, size_t bytes, void *stream) {
     return LCFIR_OK;
 }
 
+int lcfir_memcpy_d2h_async(void *dst, const void *src, size_t bytes, void *stream) {
+    if (!bytes) return LCFIR_OK;
+    if (!dst || !src) return fail(LCFIR_EINVAL, "null argument");
+    LCFIR_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost,
+                             reinterpret_cast<hipStream_t>(stream)));
+    return LCFIR_OK;
+}
+
+int lcfir_host_malloc(size_t bytes, void **out) {
+    if (!out) return fail(LCFIR_EINVAL, "out is null");
+    *out = nullptr;
+    if (hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess)
+        return fail(LCFIR_ENOMEM, "hipHostMalloc(%zu) failed", bytes);
+    return LCFIR_OK;
+}
+
+int lcfir_host_free(void *p) {
+    if (p) LCFIR_HIP(hipHostFree(p));
+    return LCFIR_OK;
+}
+
 int lcfir_stream_create(int device, void **stream) {
     if (!stream) return fail(LCFIR_EINVAL, "stream is null");
     DeviceGuard g(device);

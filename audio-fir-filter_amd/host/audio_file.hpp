@@ -19,6 +19,8 @@
 #include <cstdint>
 #include <cstring>
 #include <fstream>
+#include <functional>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -29,7 +31,9 @@ namespace lcfir_host {
 
 struct AudioFile {
     enum class Kind { Wave, Aiff } kind = Kind::Wave;
-    std::vector<uint8_t> bytes; // the whole file
+    std::shared_ptr<uint8_t> storage; // the whole file (vector- or pinned-backed)
+    uint8_t *data = nullptr;
+    size_t size = 0;
     int channels = 0;
     int64_t frames = 0;
     double sample_rate = 0.0;
@@ -59,7 +63,22 @@ public:
     using std::runtime_error::runtime_error;
 };
 
+// Where read_audio_file puts the file: a plain heap buffer, or (the lowcut
+// pipeline) pinned host memory so H2D/D2H run asynchronously.
+using Allocator = std::function<std::shared_ptr<uint8_t>(size_t)>;
+
+inline std::shared_ptr<uint8_t> heap_alloc(size_t n) {
+    return std::shared_ptr<uint8_t>(new uint8_t[n ? n : 1], std::default_delete<uint8_t[]>());
+}
+
 namespace detail {
+struct ByteView {
+    const uint8_t *p;
+    size_t n;
+    size_t size() const { return n; }
+    const uint8_t &operator[](size_t i) const { return p[i]; }
+};
+
 inline uint32_t le32(const uint8_t *p) { return p[0] | p[1] << 8 | p[2] << 16 | (uint32_t)p[3] << 24; }
 inline uint16_t le16(const uint8_t *p) { return (uint16_t)(p[0] | p[1] << 8); }
 inline uint32_t be32(const uint8_t *p) { return (uint32_t)p[0] << 24 | p[1] << 16 | p[2] << 8 | p[3]; }
@@ -86,7 +105,7 @@ inline int pcm_int_format(int bits, bool be) {
 }
 
 inline void parse_wave(AudioFile &f) {
-    const auto &b = f.bytes;
+    const ByteView b{f.data, f.size};
     size_t pos = 12;
     bool have_fmt = false, have_data = false;
     int tag = 0, bits = 0;
@@ -119,7 +138,7 @@ inline void parse_wave(AudioFile &f) {
 }
 
 inline void parse_aiff(AudioFile &f, bool aifc) {
-    const auto &b = f.bytes;
+    const ByteView b{f.data, f.size};
     size_t pos = 12;
     bool have_comm = false, have_ssnd = false;
     int bits = 0;
@@ -158,12 +177,17 @@ inline void parse_aiff(AudioFile &f, bool aifc) {
 }
 } // namespace detail
 
-inline AudioFile read_audio_file(const std::string &path) {
-    std::ifstream in(path, std::ios::binary);
+inline AudioFile read_audio_file(const std::string &path, const Allocator &alloc = heap_alloc) {
+    std::ifstream in(path, std::ios::binary | std::ios::ate);
     if (!in) throw std::runtime_error("cannot open " + path);
     AudioFile f;
-    f.bytes.assign(std::istreambuf_iterator<char>(in), std::istreambuf_iterator<char>());
-    const auto &b = f.bytes;
+    f.size = (size_t)in.tellg();
+    f.storage = alloc(f.size);
+    f.data = f.storage.get();
+    in.seekg(0);
+    if (f.size && !in.read(reinterpret_cast<char *>(f.data), (std::streamsize)f.size))
+        throw std::runtime_error("read failed: " + path);
+    const detail::ByteView b{f.data, f.size};
     if (b.size() < 12) throw FormatError("file too short: " + path);
     const std::string riff(reinterpret_cast<const char *>(&b[0]), 4);
     const std::string kind(reinterpret_cast<const char *>(&b[8]), 4);
@@ -185,10 +209,10 @@ inline AudioFile read_audio_file(const std::string &path) {
     return f;
 }
 
-inline void write_bytes(const std::string &path, const std::vector<uint8_t> &bytes) {
+inline void write_bytes(const std::string &path, const uint8_t *data, size_t size) {
     std::ofstream out(path, std::ios::binary | std::ios::trunc);
     if (!out) throw std::runtime_error("cannot create " + path);
-    out.write(reinterpret_cast<const char *>(bytes.data()), (std::streamsize)bytes.size());
+    out.write(reinterpret_cast<const char *>(data), (std::streamsize)size);
     if (!out) throw std::runtime_error("write failed: " + path);
 }
 

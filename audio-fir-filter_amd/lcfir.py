@@ -74,6 +74,9 @@ _SIGNATURES = {
     "lcfir_dev_free": ([_vp], _c_int),
     "lcfir_memcpy_h2d": ([_vp, _vp, ctypes.c_size_t, _vp], _c_int),
     "lcfir_memcpy_d2h": ([_vp, _vp, ctypes.c_size_t, _vp], _c_int),
+    "lcfir_memcpy_d2h_async": ([_vp, _vp, ctypes.c_size_t, _vp], _c_int),
+    "lcfir_host_malloc": ([ctypes.c_size_t, ctypes.POINTER(_vp)], _c_int),
+    "lcfir_host_free": ([_vp], _c_int),
     "lcfir_stream_create": ([_c_int, ctypes.POINTER(_vp)], _c_int),
     "lcfir_stream_destroy": ([_vp], _c_int),
     "lcfir_stream_sync": ([_vp], _c_int),

@@ -167,7 +167,14 @@ int lcfir_encode_pcm_dev(const float *d_in, int64_t in_stride, int32_t nch, int6
 int lcfir_dev_malloc(int device, size_t bytes, void **out);
 int lcfir_dev_free(void *p);
 int lcfir_memcpy_h2d(void *dst, const void *src, size_t bytes, void *stream);
-int lcfir_memcpy_d2h(void *dst, const void *src, size_t bytes, void *stream);
+int lcfir_memcpy_d2h(void *dst, const void *src, size_t bytes, void *stream); /* synchronous */
+/* Pinned (page-locked) host memory: H2D/D2H from it run asynchronously at PCIe rate, so a
+ * multi-file driver can overlap file i+1's upload and file i-1's download with file i's
+ * filtering.  lcfir_memcpy_d2h_async returns once the copy is queued;
+ * the caller syncs the stream before touching dst. */
+int lcfir_host_malloc(size_t bytes, void **out);
+int lcfir_host_free(void *p);
+int lcfir_memcpy_d2h_async(void *dst, const void *src, size_t bytes, void *stream);
 int lcfir_stream_create(int device, void **stream);
 int lcfir_stream_destroy(void *stream);
 int lcfir_stream_sync(void *stream);

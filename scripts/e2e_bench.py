@@ -1,0 +1,76 @@
+"""End-to-end rate of the lowcut tool: WAVE files on disk -> pinned host ->
+PCIe -> decode/filter/normalize/encode on the GPU -> PCIe -> disk, pipelined
+across files (read / 2 GPU streams / write).  This is the PCIe- and disk-
+inclusive number DESIGN.md quotes beside bench.py's HBM-resident `value`.
+
+usage: python scripts/e2e_bench.py [--files 4] [--minutes 10] [--out gpurun_out/e2e.json]
+Inputs are config-2-shaped synthetic files (stereo 48 kHz int24, SURVEY.md s8d
+generator), written to $TMPDIR.
+"""
+import argparse
+import json
+import os
+import re
+import shutil
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "audio-fir-filter_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import synth  # noqa: E402
+import pcm_ref  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--files", type=int, default=4)
+    ap.add_argument("--minutes", type=float, default=10.0)
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "e2e.json"))
+    a = ap.parse_args()
+    rate, nch = 48000, 2
+    n = int(a.minutes * 60 * rate)
+    work = tempfile.mkdtemp(prefix="lcfir_e2e_")
+    try:
+        paths = []
+        t0 = time.time()
+        for i in range(a.files):
+            x = synth.file_buffer(nch, n, float(rate), file=i, bits=24)
+            p = os.path.join(work, f"f{i}.wav")
+            pcm_ref.write_wave(p, x, rate, "s24le")
+            paths.append(p)
+            del x
+        gen_s = time.time() - t0
+        exe = os.path.join(ROOT, "audio-fir-filter_amd", "lowcut")
+        out_dir = os.path.join(work, "out")
+        t0 = time.time()
+        r = subprocess.run([exe, "--timing", "-f", "20", "-s", "48", *paths, out_dir],
+                           capture_output=True, text=True, timeout=1200)
+        wall = time.time() - t0
+        if r.returncode != 0:
+            sys.exit(f"lowcut failed: {r.stderr}")
+        m = re.search(r"timing total: (\d+) file\(s\), ([\d.]+) s, ([\d.]+) Msamples/s", r.stdout)
+        per_file = re.findall(r"timing (\S+): read ([\d.]+) s, gpu ([\d.]+) s .*write ([\d.]+) s",
+                              r.stdout)
+        res = {
+            "what": "lowcut end to end (disk + pinned host + PCIe + GPU), pipelined across files",
+            "files": a.files, "minutes_per_file": a.minutes, "format": "stereo 48 kHz s24le WAVE",
+            "ntaps": 4001, "samples": a.files * nch * n,
+            "tool_seconds": float(m.group(2)), "msamples_per_s": float(m.group(3)),
+            "process_wall_seconds": wall, "input_generation_seconds": gen_s,
+            "per_file": [{"file": f, "read_s": float(rd), "gpu_s": float(g), "write_s": float(w)}
+                         for f, rd, g, w in per_file],
+        }
+        os.makedirs(os.path.dirname(a.out), exist_ok=True)
+        with open(a.out, "w") as fh:
+            json.dump(res, fh, indent=1)
+        print(json.dumps(res))
+    finally:
+        shutil.rmtree(work, ignore_errors=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -22,7 +22,7 @@ step pytest_gpu 1200 python -m pytest tests -m gpu -x -q
 step bench 600 python bench.py --steps 20 --warmup 3 "$@"
 cd /tmp && export TMPDIR=/tmp
 step rocprof 600 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof_$TAG" -o bench -- \
-    python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --no-parity "$@"
+    python3 "$ROOT/bench.py" --steps 20 --warmup 3 --no-cpu-baseline --no-parity "$@"
 cp "$OUT/prof_$TAG/bench_kernel_stats.csv" "$OUT/kernel_stats_$TAG.csv"
 for c in FETCH_SIZE WRITE_SIZE; do
     step "pmc_$c" 600 rocprofv3 --pmc $c --kernel-include-regex 'fir_' -f csv \
