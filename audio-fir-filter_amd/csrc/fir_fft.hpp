@@ -4,63 +4,129 @@
 // padding outside [0,N), outputs [start,end), RNE to f32), evaluated with
 // f64 FFTs instead of T multiply-adds per sample.
 //
-// One workgroup = one segment of B = L - T + 1 consecutive outputs:
+// One unit = one segment of B = L - T + 1 consecutive outputs:
 //   x_seg[i] = x[n0 - half + i], i in [0, L), L = 16384 real samples
 //   c = IFFT_L( FFT_L(x_seg) * G ),  G = FFT_L(reversed taps, zero padded)
 //   y[n0 + m - (T-1)] = c[m] for m in [T-1, L)          (overlap-save)
-// The real length-L transform is done as one complex M = L/2 = 8192-point FFT
-// of z[k] = x[2k] + i x[2k+1] with the even/odd split/merge fused into a
-// single "pair" pass that also multiplies by G; the inverse uses the conj
-// trick (IFFT(V) = conj(FFT(conj(V)))), so one forward Stockham kernel body
-// (radix 16, 16, 16, 2) serves both directions.  All scale factors (the two
-// 1/2 of the split/merge and the 1/M of the inverse) are folded into G, which
-// the host computes once per filter in long double.
+// The real length-L transform is one complex M = L/2 = 8192-point FFT of
+// z[m] = x_seg[2m] + i x_seg[2m+1]; the even/odd split and merge are fused
+// with the multiply by G into one "pair" step on bins k and M-k; the inverse
+// is conj(FFT(conj(V))).  All scale factors live in the pair table.
 //
-// Layout: the complex work array (8192 x 16 B = 128 KiB) lives in LDS with
-// one pad slot per 16 entries (139 KiB), so one 512-thread workgroup fits a
-// CU (2 waves per SIMD); each thread owns 16 complex values per pass.  The
-// grid is persistent (one workgroup per CU looping over (channel, segment)
-// units).  Samples are read and results written through range-checked raw
-// buffer resources, so the zero padding at the channel edges and the output
-// range clipping need no branches.  Twiddles of the inner passes come from a
-// 1024-entry W_16384 table (L1-resident) raised to the needed powers in
-// registers by a short odd/even product chain.
-//
-// Measured (profiles/): VALU ~25 %, LDS ~20 % busy; the
-// binding cost is the barrier-serialised read -> compute -> write phases of
-// the eight Stockham passes.  Persistence, prefetching the next unit's
-// samples and hoisting the pair-pass loads were each measured neutral or
-// negative; the next step is wave-local exchanges (fewer block barriers).
+// Four-step decomposition, M = 16 x 512 (index flow, lane
+// tables and LDS bank patterns are checked by scripts/fft_lds_sim.py):
+//   stage 1 (thread b of 512): 16-point DFT over z[512 a + b] -> column c,
+//           times W_8192^(b c); one workgroup-wide transpose into LDS column
+//           blocks [c][b];
+//   wave w owns the two columns {w, 16-w} (wave 0: {0, 8}) and does their
+//           512-point DFTs as 8 x 8 x 8 with two wave-local LDS exchanges --
+//           no workgroup barrier;
+//   the lane assignment of the last exchange is mirrored between a wave's two
+//           columns, so bins k and M-k sit in the same lane: the pair step runs
+//           in registers (wave 0 needs one lane, kFftSpecialLane, permuted);
+//   the inverse runs the same stages in transposed order and ends with one
+//           workgroup-wide transpose and the 16-point DFTs.
+// Per segment: 3 workgroup barriers and 6 LDS round trips of the 128 KiB work
+// array (the radix-16x16x16x2 Stockham form it replaces needed 14 barriers and
+// ~8 round trips).  The grid is persistent (one 512-thread workgroup per CU);
+// samples are read and results written through range-checked raw buffer
+// resources, so the channel-edge zero padding and output clipping need no
+// branches.
 #pragma once
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cmath>
+#include <cstdint>
 #include <cstdlib>
 #include <string>
 #include <vector>
 
 #include "fir_direct.hpp"
 
+// Phase timestamps for tools/fft_trace.hip (off in the product build): lane 0
+// of every wave of workgroups < 64 records s_memtime at each phase boundary of
+// its 5th unit.
+#ifdef LCFIR_FFT_TRACE
+__device__ unsigned long long g_fft_trace[64][8][24];
+#define FFT_STAMP(i)                                                                     \
+    do {                                                                                 \
+        if (blockIdx.x < 64 && u == (int64_t)blockIdx.x + 4 * (int64_t)gridDim.x &&      \
+            (threadIdx.x & 63) == 0)                                                     \
+            g_fft_trace[blockIdx.x][threadIdx.x >> 6][i] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define FFT_STAMP(i) \
+    do {             \
+    } while (0)
+#endif
+
+#ifndef LCFIR_FFT_PREFETCH
+#define LCFIR_FFT_PREFETCH 1
+#endif
+#ifndef LCFIR_FFT_TWLDS
+#define LCFIR_FFT_TWLDS 1
+#endif
+#ifndef LCFIR_FFT_PAIRHOIST
+#define LCFIR_FFT_PAIRHOIST 1
+#endif
+
 namespace lcfir {
 
 constexpr int kFftL = 16384;        // real segment length
 constexpr int kFftM = kFftL / 2;    // complex FFT length
 constexpr int kFftNT = 512;         // threads per workgroup
-constexpr int kFftTwN = 1024;       // entries of the W_L twiddle table
 constexpr int kFftMinB = 2048;      // smallest useful segment (B = L - T + 1)
+constexpr int kFftTw = 512 + 64;    // twiddles: W_8192^i (i < 512), W_512^i (i < 64)
+constexpr int kFftPairSlots = 9;    // pair-table slots per thread (8 pairs + k = M/2)
+constexpr int kFftSpecialLane = 35; // wave-0 lane holding the self-paired bins 0 and M/2
+
+// Wave 0, lanes 32..63: the column-0 task pairs (d1A | e1A << 3 | d1B << 6 |
+// e1B << 9), ordered so the exchange-2 reads and exchange-3 writes stay
+// bank-conflict free (generated and checked by scripts/fft_lds_sim.py).
+constexpr uint16_t kFftWave0C0[32] = {
+    0xf43, 0x99a, 0xfc1, 0x020, 0x4ed, 0xe47, 0xc8e, 0xb14, 0x89e, 0xec5, 0x85f,
+    0xd0c, 0x373, 0x3f1, 0xc10, 0x5aa, 0xb92, 0x91c, 0xe86, 0xad5, 0xa18, 0x95b,
+    0x5e9, 0x46f, 0xf82, 0xe08, 0x8dd, 0x2b6, 0xf04, 0xd4b, 0x9d9, 0x277};
 
 struct FftPlan {
     bool ready = false;
     int ntaps = 0;
     int B = 0;
-    double2 *d_G = nullptr;  // M + 1 bins, scaled by 1 / (4M)
-    double2 *d_tw = nullptr; // W_L^i, i in [0, kFftTwN)
-    int cus = 256;           // compute units of the plan's device (persistent grid)
+    double2 *d_pair = nullptr; // [3][kFftPairSlots][512]: G[k], G[M-k], W_L^k per (slot, thread)
+    double2 *d_tw = nullptr;   // kFftTw twiddles
+    uint32_t *d_task = nullptr; // [512] task words (cA, d1A, e1A, cB, d1B, e1B)
+    int cus = 256;             // compute units of the plan's device (persistent grid)
 };
 
 inline bool fft_supported(int ntaps) { return ntaps >= 1 && kFftL - ntaps + 1 >= kFftMinB; }
 inline bool fft_preferred(int ntaps) { return ntaps >= 96 && fft_supported(ntaps); }
+
+// Task word of thread t = 64 w + lane after exchange 2: task A = (cA, d1A, e1A),
+// task B = (cB, d1B, e1B); bins k = c + 16 (d1 + 8 e1 + 64 e2), e2 = register.
+// Waves 1..7: columns w and 16 - w, B mirrors A, so X[k] (A[e2]) and X[M-k]
+// (B[7-e2]) share a lane.  Wave 0: lanes 0..31 column-8 mirror pairs, lanes
+// 32..63 column-0 partner pairs (kFftWave0C0).
+inline uint32_t fft_task_word(int t) {
+    const int w = t >> 6, lane = t & 63;
+    int ca, da, ea, cb, db, eb;
+    if (w != 0 || lane < 32) {
+        ca = w ? w : 8;
+        cb = w ? 16 - w : 8;
+        da = lane & 7;
+        ea = lane >> 3;
+        db = 7 - da;
+        eb = 7 - ea;
+    } else {
+        const int v = kFftWave0C0[lane - 32];
+        ca = cb = 0;
+        da = v & 7;
+        ea = (v >> 3) & 7;
+        db = (v >> 6) & 7;
+        eb = (v >> 9) & 7;
+    }
+    return (uint32_t)(ca | da << 4 | ea << 7 | cb << 10 | db << 14 | eb << 17);
+}
 
 // ---------------------------------------------------------------------------
 // device helpers
@@ -77,8 +143,6 @@ __device__ __forceinline__ double2 cmulc(double2 a, double2 b) {
 }
 __device__ __forceinline__ double2 mul_mi(double2 a) { return make_double2(a.y, -a.x); } // * (-i)
 __device__ __forceinline__ double2 mul_pi(double2 a) { return make_double2(-a.y, a.x); } // * (+i)
-
-__device__ __forceinline__ int fpad(int i) { return i + (i >> 4); }
 
 constexpr double kC1 = 0.92387953251128675613; // cos(pi/8)
 constexpr double kS1 = 0.38268343236508977173; // sin(pi/8)
@@ -133,8 +197,49 @@ __device__ __forceinline__ void dft16(double2 (&a)[16]) {
     for (int i = 0; i < 16; ++i) a[i] = t[i];
 }
 
-// w[r] = w1^r for r = 1..15 by a product tree (depth <= 4)
-__device__ __forceinline__ void twiddle_powers(double2 w1, double2 (&w)[16]) {
+
+// forward 8-point DFT, natural order in and out (radix-2 x 4)
+__device__ __forceinline__ void dft8(double2 (&a)[8]) {
+    double2 b[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        b[k] = cadd(a[k], a[k + 4]);
+        b[k + 4] = csub(a[k], a[k + 4]);
+    }
+    b[5] = w16<2>(b[5]); // W8^1
+    b[6] = mul_mi(b[6]); // W8^2
+    b[7] = w16<6>(b[7]); // W8^3
+    dft4(b[0], b[1], b[2], b[3]);
+    dft4(b[4], b[5], b[6], b[7]);
+    a[0] = b[0];
+    a[2] = b[1];
+    a[4] = b[2];
+    a[6] = b[3];
+    a[1] = b[4];
+    a[3] = b[5];
+    a[5] = b[6];
+    a[7] = b[7];
+}
+
+// a[r] *= w1^r, r = 1..15, powers by an odd/even chain (w^(2i+1) = w^(2i-1) w^2):
+// 4 live values, <= 8 products deep (error ~1e-15)
+__device__ __forceinline__ void twiddle16(double2 (&a)[16], double2 w1) {
+    const double2 w2 = cmul(w1, w1);
+    double2 wo = w1, we = w2;
+    a[1] = cmul(a[1], wo);
+    a[2] = cmul(a[2], we);
+#pragma unroll
+    for (int r = 3; r < 15; r += 2) {
+        wo = cmul(wo, w2);
+        we = cmul(we, w2);
+        a[r] = cmul(a[r], wo);
+        a[r + 1] = cmul(a[r + 1], we);
+    }
+    a[15] = cmul(a[15], cmul(wo, w2));
+}
+
+// w[r] = w1^r, r = 1..7 (depth <= 3)
+__device__ __forceinline__ void powers8(double2 w1, double2 (&w)[8]) {
     w[1] = w1;
     w[2] = cmul(w1, w1);
     w[3] = cmul(w[2], w1);
@@ -142,78 +247,31 @@ __device__ __forceinline__ void twiddle_powers(double2 w1, double2 (&w)[16]) {
     w[5] = cmul(w[4], w1);
     w[6] = cmul(w[4], w[2]);
     w[7] = cmul(w[4], w[3]);
-    w[8] = cmul(w[4], w[4]);
-#pragma unroll
-    for (int r = 9; r < 16; ++r) w[r] = cmul(w[8], w[r - 8]);
 }
 
-// Second half of a Stockham radix-16 pass (N = 8192, 512 butterflies, one per
-// thread): twiddle, DFT16, store to LDS in expanded order.
-template <int NS>
-__device__ __forceinline__ void r16_finish(double2 (&a)[16], double2 *lds, int j, double2 w1) {
-    if constexpr (NS > 1) {
-        // w1 = W_{NS*16}^(j % NS); element r is multiplied by w1^r.  Powers by
-        // an odd/even chain (w^(2i+1) = w^(2i-1) w^2): 4 live values instead of
-        // a 15-entry table, <= 8 products deep (error ~1e-15).
-        const double2 w2 = cmul(w1, w1);
-        double2 wo = w1, we = w2;
-        a[1] = cmul(a[1], wo);
-        a[2] = cmul(a[2], we);
+__device__ __forceinline__ void twiddle8(double2 (&a)[8], const double2 (&w)[8]) {
 #pragma unroll
-        for (int r = 3; r < 15; r += 2) {
-            wo = cmul(wo, w2);
-            we = cmul(we, w2);
-            a[r] = cmul(a[r], wo);
-            a[r + 1] = cmul(a[r + 1], we);
-        }
-        a[15] = cmul(a[15], cmul(wo, w2));
-    }
-    dft16(a);
-    const int idx = (j / NS) * NS * 16 + (j % NS);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) lds[fpad(idx + r * NS)] = a[r];
+    for (int r = 1; r < 8; ++r) a[r] = cmul(a[r], w[r]);
 }
 
-template <int NS>
-__device__ __forceinline__ void r16_pass(double2 *lds, int j, double2 w1) {
-    double2 a[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) a[r] = lds[fpad(j + r * (kFftM / 16))];
-    __syncthreads(); // every read of this pass before any write (in place)
-    r16_finish<NS>(a, lds, j, w1);
-    __syncthreads();
+// The wave-local exchanges: LDS operations of one wave execute in order, so
+// only the compiler must be kept from moving them across (rocPRIM's
+// wave_barrier idiom).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// constant W_16^q and W_32^q (forward)
-__device__ __forceinline__ double2 w16q(int q) {
-    constexpr double c[8] = {1.0, kC1, kR2, kS1, 0.0, -kS1, -kR2, -kC1};
-    constexpr double s[8] = {0.0, kS1, kR2, kC1, 1.0, kC1, kR2, kS1};
-    return make_double2(c[q], -s[q]);
+// LDS layouts inside one column block of 512 (index in 16-B units); XOR
+// swizzles keep every exchange bank-conflict free (scripts/fft_lds_sim.py)
+__device__ __forceinline__ int fx1(int l, int d1) { return 64 * d1 + (l ^ (8 * d1)); }
+__device__ __forceinline__ int fx2(int l1, int d1, int e1) {
+    return 64 * e1 + 8 * d1 + (l1 ^ (((d1 >> 1) & 1) | ((e1 & 3) << 1)));
 }
-
-__device__ __forceinline__ double2 w32q(int q) {
-    constexpr double c[8] = {1.0, 0.98078528040323044913, kC1, 0.83146961230254523708,
-                             kR2, 0.55557023301960222474, kS1, 0.19509032201612826785};
-    constexpr double s[8] = {0.0, 0.19509032201612826785, kS1, 0.55557023301960222474,
-                             kR2, 0.83146961230254523708, kC1, 0.98078528040323044913};
-    return make_double2(c[q], -s[q]);
-}
-
-// Final radix-2 pass (NS = 4096) of the 8192-point transform: thread j owns
-// butterflies b = j + 512 q, q < 8; lo[q] = X[b], hi[q] = X[b + 4096].
-__device__ __forceinline__ void r2_pass(const double2 *lds, int j, double2 wj /* W_8192^j */,
-                                        double2 (&lo)[8], double2 (&hi)[8]) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        const int b = j + 512 * q;
-        const double2 v0 = lds[fpad(b)];
-        double2 v1 = lds[fpad(b + kFftM / 2)];
-        // W_8192^b = W_8192^j * W_16^q
-        const double2 w = (q == 0) ? wj : cmul(wj, w16q(q));
-        v1 = cmul(v1, w);
-        lo[q] = cadd(v0, v1);
-        hi[q] = csub(v0, v1);
-    }
+__device__ __forceinline__ int fx3(int d1, int e1, int b0) { return 64 * e1 + 8 * b0 + d1; }
+__device__ __forceinline__ int fx4(int d1, int b0, int g0) {
+    return 64 * g0 + 8 * b0 + (d1 ^ (((b0 >> 1) & 1) | ((g0 & 3) << 1)));
 }
 
 // Split/merge of the real transform fused with the filter multiply.
@@ -245,97 +303,333 @@ __device__ __forceinline__ void fft_load_unit(const DirectParams &p, int ch, int
     const float *x = p.x + (int64_t)ch * p.x_stride;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float *>(x), (short)0, (int)((p.x_hi - p.x_lo) * 4), 0x00020000);
-    const int off0 = (int)((n0 - p.half - p.x_lo) * 4) + 8 * j; // may be negative
+    const int64_t w0 = n0 - p.half - p.x_lo; // window start inside the loaded range
+    const int off0 = (int)(w0 * 4) + 8 * j;   // may be negative
+    if (w0 >= 0 && w0 + kFftL <= p.x_hi - p.x_lo) {
+        // interior unit (all but the first and last of a range): plain cached
+        // loads, which the compiler may merge into dwordx2
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int off = off0 + 8 * 512 * r;
-        // aux bit 31 = volatile: keeps the two dword loads from being merged
-        // into one dwordx2, whose range check is all-or-nothing (a pair
-        // straddling the window start would lose its in-range sample)
-        v[r].x = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, (int)0x80000000));
-        v[r].y = __int_as_float(
-            __builtin_amdgcn_raw_buffer_load_b32(rsrc, off + 4, 0, (int)0x80000000));
+        for (int r = 0; r < 16; ++r) {
+            const int off = off0 + 8 * 512 * r;
+            v[r].x = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, 0));
+            v[r].y = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, off + 4, 0, 0));
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int off = off0 + 8 * 512 * r;
+            // aux bit 31 = volatile: keeps the two dword loads from being merged
+            // into one dwordx2, whose range check is all-or-nothing (a pair
+            // straddling the window start would lose its in-range sample)
+            v[r].x = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, (int)0x80000000));
+            v[r].y = __int_as_float(
+                __builtin_amdgcn_raw_buffer_load_b32(rsrc, off + 4, 0, (int)0x80000000));
+        }
     }
 }
 
+// Wave max of a running peak, one atomic per wave (channel ch < 0: nothing yet).
+__device__ __forceinline__ void fft_peak_flush(const DirectParams &p, int ch, float pk) {
+    if (!p.peak || ch < 0) return;
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) pk = fmaxf(pk, __shfl_xor(pk, s, 64));
+    if ((threadIdx.x & 63) == 0) atomicMax(p.peak + ch * p.peak_stride, __float_as_uint(pk));
+}
+
 // Persistent: one workgroup per CU walks the units u = blockIdx.x + i * gridDim.x
-// of the nch x nseg (channel, segment) grid, so no CU idles between workgroup
-// dispatches.
-__global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, const double2 *__restrict__ G,
-                                                            const double2 *__restrict__ tw, int B,
+// of the nch x nseg (channel, segment) grid.  The next unit's samples are
+// loaded during the current unit's inverse, so HBM latency is off the path.
+__global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, const double2 *__restrict__ pair,
+                                                            const double2 *__restrict__ tw,
+                                                            const uint32_t *__restrict__ task, int B,
                                                             int64_t nseg, int64_t units) {
     extern __shared__ double2 flds[];
+    double2 *twl = flds + kFftM; // the kFftTw twiddles, LDS-resident
+#if LCFIR_FFT_TWLDS
+#define TWL(i) twl[i]
+    for (int i = threadIdx.x; i < kFftTw; i += kFftNT) twl[i] = tw[i];
+#else
+#define TWL(i) tw[i]
+#endif
+    float2 v[16]; // samples of the unit about to start
+#if LCFIR_FFT_PREFETCH
+    {
+        const int64_t u = blockIdx.x;
+        fft_load_unit(p, (int)(u / nseg), p.start + (u % nseg) * B, threadIdx.x, v);
+    }
+#endif
+    __syncthreads();
+    float pk_run = 0.0f; // running max |y| of channel pk_ch over this lane's outputs
+    int pk_ch = -1;
     for (int64_t u = blockIdx.x; u < units; u += gridDim.x) {
-    // Laundered thread index: everything derived from it (twiddles, LDS
-    // addresses) is recomputed per unit instead of being hoisted out of the
-    // loop, which would keep hundreds of values live and spill.
+    // Laundered thread index: everything derived from it is recomputed per
+    // unit instead of being hoisted out of the loop (keeps pressure down).
     int j = threadIdx.x;
     asm volatile("" : "+v"(j));
+    const int lane = j & 63;
+    const int w = j >> 6;
+    const int col0 = w == 0 ? 0 : w;        // the wave's two columns
+    const int col1 = w == 0 ? 8 : 16 - w;
+    double2 *blk0 = flds + 512 * col0;
+    double2 *blk1 = flds + 512 * col1;
     const int ch = (int)(u / nseg);
     const int64_t n0 = p.start + (u % nseg) * B;
+    FFT_STAMP(0);
 
-    // ---- forward pass 1 (NS = 1): z[m] = (x_seg[2m], x_seg[2m+1]), m = j + 512 r
+    // ---- stage 1: thread b = j, 16-point DFT over z[512 a + b] -> column c
     {
-        float2 v[16];
+#if !LCFIR_FFT_PREFETCH
         fft_load_unit(p, ch, n0, j, v);
+#endif
         double2 a[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) a[r] = make_double2((double)v[r].x, (double)v[r].y);
-        r16_finish<1>(a, flds, j, make_double2(1.0, 0.0));
-        __syncthreads();
-    }
-    r16_pass<16>(flds, j, tw[2 * ((j % 16) * (kFftM / 256))]);
-    r16_pass<256>(flds, j, tw[2 * ((j % 256) * (kFftM / 4096))]);
-
-    // ---- forward radix-2 pass; upper half goes to LDS for the partner thread
-    double2 lo[8], hi[8];
-    r2_pass(flds, j, tw[2 * j], lo, hi);
+        dft16(a);
+        twiddle16(a, TWL(j)); // W_8192^(b c)
+        FFT_STAMP(1);
+        __syncthreads();     // the previous unit's last reads are done
+        FFT_STAMP(2);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) flds[fpad(j + 512 * q + kFftM / 2)] = hi[q];
-    __syncthreads();
+        for (int c = 0; c < 16; ++c) flds[512 * c + j] = a[c];
+        FFT_STAMP(3);
+        __syncthreads();
+        FFT_STAMP(4);
+    }
 
-    // ---- pair pass: V[k], V[M-k] for k = j + 512 q (< M/2), plus k = M/2 (thread 0)
+    double2 x0[8], x1[8]; // the wave's two columns (later: tasks A and B)
+    double2 tws[8];
+    // ---- stage A: lane l holds b = l + 64 t; radix-8 over t -> d1; * W_512^(l d1)
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        x0[t] = blk0[lane + 64 * t];
+        x1[t] = blk1[lane + 64 * t];
+    }
+    dft8(x0);
+    dft8(x1);
+    powers8(TWL(512 + lane), tws);
+    twiddle8(x0, tws);
+    twiddle8(x1, tws);
+    FFT_STAMP(5);
+    wave_lds_sync();
+#pragma unroll
+    for (int d1 = 0; d1 < 8; ++d1) {
+        blk0[fx1(lane, d1)] = x0[d1];
+        blk1[fx1(lane, d1)] = x1[d1];
+    }
+    wave_lds_sync();
+    FFT_STAMP(6);
+    // ---- stage B: lane (l1, d1) gathers l2; radix-8 -> e1; * W_64^(l1 e1)
     {
-        const double2 wj = tw[j]; // W_L^j
+        const int l1 = lane & 7, d1 = lane >> 3;
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const int k = j + 512 * q;
-            const double2 Zk = lo[q];
-            const double2 Zmk = (k == 0) ? Zk : flds[fpad(kFftM - k)];
-            // W_L^k = W_L^j * W_32^q
-            const double2 W = (q == 0) ? wj : cmul(wj, w32q(q));
-            double2 Vk, Vmk;
-            pair_step(Zk, Zmk, W, G[k], G[kFftM - k], Vk, Vmk);
-            flds[fpad(k)] = Vk;
-            if (k != 0) flds[fpad(kFftM - k)] = Vmk;
+        for (int l2 = 0; l2 < 8; ++l2) {
+            x0[l2] = blk0[fx1(l1 + 8 * l2, d1)];
+            x1[l2] = blk1[fx1(l1 + 8 * l2, d1)];
         }
-        if (j == 0) {
-            const int k = kFftM / 2;
-            const double2 Zk = flds[fpad(k)];
-            double2 Vk, Vmk;
-            pair_step(Zk, Zk, make_double2(0.0, -1.0), G[k], G[k], Vk, Vmk);
-            flds[fpad(k)] = Vk;
+        dft8(x0);
+        dft8(x1);
+        powers8(TWL(512 + 8 * l1), tws);
+        twiddle8(x0, tws);
+        twiddle8(x1, tws);
+        FFT_STAMP(7);
+        wave_lds_sync();
+#pragma unroll
+        for (int e1 = 0; e1 < 8; ++e1) {
+            blk0[fx2(l1, d1, e1)] = x0[e1];
+            blk1[fx2(l1, d1, e1)] = x1[e1];
         }
+        wave_lds_sync();
+        FFT_STAMP(8);
     }
-    __syncthreads();
-
-    // ---- inverse: conj(FFT(conj(V)))
+#if LCFIR_FFT_PAIRHOIST
+    // ---- pair-table loads, issued ahead of stage C (L2 latency off the path)
+    double2 pg[8], pgm[8];
+    const double2 g4 = pair[512 * 8 + j]; // G[M/2]: used by the special lane only
     {
-        double2 a[16];
+        const double2 *t0 = pair + j, *t1 = pair + kFftPairSlots * 512 + j;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) a[r] = cconj(flds[fpad(j + 512 * r)]);
-        __syncthreads();
-        r16_finish<1>(a, flds, j, make_double2(1.0, 0.0));
-        __syncthreads();
+        for (int i = 0; i < 8; ++i) {
+            pg[i] = t0[512 * i];
+            pgm[i] = t1[512 * i];
+        }
     }
-    r16_pass<16>(flds, j, tw[2 * ((j % 16) * (kFftM / 256))]);
-    r16_pass<256>(flds, j, tw[2 * ((j % 256) * (kFftM / 4096))]);
-    r2_pass(flds, j, tw[2 * j], lo, hi);
+#endif
+    // ---- stage C: per task, radix-8 over l1 -> e2: x0[e2] = X[kA], x1[e2] = X[kB]
+    const uint32_t tk = task[j];
+    const int cA = tk & 15, dA = (tk >> 4) & 7, eA = (tk >> 7) & 7;
+    const int cB = (tk >> 10) & 15, dB = (tk >> 14) & 7, eB = (tk >> 17) & 7;
+    {
+        const double2 *ba = flds + 512 * cA, *bb = flds + 512 * cB;
+#pragma unroll
+        for (int l1 = 0; l1 < 8; ++l1) {
+            x0[l1] = ba[fx2(l1, dA, eA)];
+            x1[l1] = bb[fx2(l1, dB, eB)];
+        }
+    }
+    dft8(x0);
+    dft8(x1);
+    FFT_STAMP(9);
+#if !LCFIR_FFT_PAIRHOIST
+    // ---- pair-table loads, issued ahead of stage C (L2 latency off the path)
+    double2 pg[8], pgm[8];
+    const double2 g4 = pair[512 * 8 + j]; // G[M/2]: used by the special lane only
+    {
+        const double2 *t0 = pair + j, *t1 = pair + kFftPairSlots * 512 + j;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            pg[i] = t0[512 * i];
+            pgm[i] = t1[512 * i];
+        }
+    }
+#endif
+    // ---- pair step in registers: pairs (x0[i], x1[7-i]); outputs conj(V)
+    {
+        const bool w0 = (w == 0); // wave-uniform
+        const bool sp = w0 && lane == kFftSpecialLane;
+        double2 b4 = x1[4];
+        if (w0) { // special lane: pairs (A_i, A_7-i), (B_1..3, B_7..5), (B_0, B_0)
+            const double2 A[8] = {x0[0], x0[1], x0[2], x0[3], x0[4], x0[5], x0[6], x0[7]};
+            const double2 Bv[8] = {x1[0], x1[1], x1[2], x1[3], x1[4], x1[5], x1[6], x1[7]};
+            x0[4] = sp ? Bv[1] : A[4];
+            x0[5] = sp ? Bv[2] : A[5];
+            x0[6] = sp ? Bv[3] : A[6];
+            x0[7] = sp ? Bv[0] : A[7];
+            x1[1] = sp ? Bv[5] : Bv[1];
+            x1[2] = sp ? Bv[6] : Bv[2];
+            x1[3] = sp ? Bv[7] : Bv[3];
+            x1[4] = sp ? A[4] : Bv[4];
+            x1[5] = sp ? A[5] : Bv[5];
+            x1[6] = sp ? A[6] : Bv[6];
+            x1[7] = sp ? A[7] : Bv[7];
+        }
+        // W_L^(k_i) = W_L^(k_0) W_16^i (k_i = k_0 + 1024 i); the special lane's
+        // list (k = 512, 1536, 2560, 3584, 1024, 2048, 3072, 0) is patched in
+        const double2 wbase = pair[2 * kFftPairSlots * 512 + j];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            double2 W = wbase;
+            if (i == 1) W = cmul(wbase, make_double2(kC1, -kS1));
+            if (i == 2) W = w16<2>(wbase);
+            if (i == 3) W = cmul(wbase, make_double2(kS1, -kC1));
+            if (i == 4) W = mul_mi(wbase);
+            if (i == 5) W = cmul(wbase, make_double2(-kS1, -kC1));
+            if (i == 6) W = w16<6>(wbase);
+            if (i == 7) W = cmul(wbase, make_double2(-kC1, -kS1));
+            if (w0 && i >= 4) { // special lane: W_16^(i-3) for i < 7, 1 for i = 7
+                const double2 ws = i == 4 ? make_double2(kC1, -kS1)
+                                 : i == 5 ? make_double2(kR2, -kR2)
+                                 : i == 6 ? make_double2(kS1, -kC1) : make_double2(1.0, 0.0);
+                W = sp ? ws : W;
+            }
+            double2 Vk, Vmk;
+            pair_step(x0[i], x1[7 - i], W, pg[i], pgm[i], Vk, Vmk);
+            x0[i] = cconj(Vk);
+            x1[7 - i] = cconj(Vmk);
+        }
+        if (w0) {
+            double2 V4, Vx;
+            pair_step(b4, b4, make_double2(0.0, -1.0), g4, g4, V4, Vx);
+            const double2 A[8] = {x0[0], x0[1], x0[2], x0[3], x0[4], x0[5], x0[6], x0[7]};
+            const double2 Bv[8] = {x1[0], x1[1], x1[2], x1[3], x1[4], x1[5], x1[6], x1[7]};
+            x0[4] = sp ? Bv[4] : A[4];
+            x0[5] = sp ? Bv[5] : A[5];
+            x0[6] = sp ? Bv[6] : A[6];
+            x0[7] = sp ? Bv[7] : A[7];
+            x1[0] = sp ? A[7] : Bv[0];
+            x1[1] = sp ? A[4] : Bv[1];
+            x1[2] = sp ? A[5] : Bv[2];
+            x1[3] = sp ? A[6] : Bv[3];
+            x1[4] = sp ? cconj(V4) : Bv[4];
+            x1[5] = sp ? Bv[1] : Bv[5];
+            x1[6] = sp ? Bv[2] : Bv[6];
+            x1[7] = sp ? Bv[3] : Bv[7];
+        }
+    }
 
-    // ---- outputs: c[2m] = Re v'[m], c[2m+1] = -Im v'[m], valid for 2m+e >= T-1
-    // Range-checked buffer over y[start, end): invalid lanes store to an
-    // out-of-range offset, which the hardware drops (no branches).  c index
-    // < T-1 belongs to the previous segment; beyond `end` is outside the range.
+    FFT_STAMP(10);
+    // ---- prefetch the next unit's samples (consumed by its stage 1)
+    if (LCFIR_FFT_PREFETCH && u + gridDim.x < units) {
+        const int64_t un = u + gridDim.x;
+        fft_load_unit(p, (int)(un / nseg), p.start + (un % nseg) * B, j, v);
+    }
+
+    FFT_STAMP(11);
+    // ---- inverse stage A': per task radix-8 over e2 -> beta0; * W_512^(beta0 d')
+    dft8(x0);
+    dft8(x1);
+    powers8(TWL(512 + dA + 8 * eA), tws);
+    twiddle8(x0, tws);
+    powers8(TWL(512 + dB + 8 * eB), tws);
+    twiddle8(x1, tws);
+    FFT_STAMP(12);
+    wave_lds_sync();
+    {
+        double2 *ba = flds + 512 * cA, *bb = flds + 512 * cB;
+#pragma unroll
+        for (int b0 = 0; b0 < 8; ++b0) {
+            ba[fx3(dA, eA, b0)] = x0[b0];
+            bb[fx3(dB, eB, b0)] = x1[b0];
+        }
+    }
+    wave_lds_sync();
+    FFT_STAMP(13);
+    // ---- stage B': lane (d1, beta0) gathers e1; radix-8 -> gamma0; * W_64^(gamma0 d1)
+    {
+        const int d1 = lane & 7, b0 = lane >> 3;
+#pragma unroll
+        for (int e1 = 0; e1 < 8; ++e1) {
+            x0[e1] = blk0[fx3(d1, e1, b0)];
+            x1[e1] = blk1[fx3(d1, e1, b0)];
+        }
+        dft8(x0);
+        dft8(x1);
+        powers8(TWL(512 + 8 * d1), tws);
+        twiddle8(x0, tws);
+        twiddle8(x1, tws);
+        FFT_STAMP(14);
+        wave_lds_sync();
+#pragma unroll
+        for (int g0 = 0; g0 < 8; ++g0) {
+            blk0[fx4(d1, b0, g0)] = x0[g0];
+            blk1[fx4(d1, b0, g0)] = x1[g0];
+        }
+        wave_lds_sync();
+        FFT_STAMP(15);
+    }
+    // ---- stage C': lane rho = beta0 + 8 gamma0 gathers d1; radix-8 -> gamma1
+    {
+        const int b0 = lane & 7, g0 = lane >> 3;
+#pragma unroll
+        for (int d1 = 0; d1 < 8; ++d1) {
+            x0[d1] = blk0[fx4(d1, b0, g0)];
+            x1[d1] = blk1[fx4(d1, b0, g0)];
+        }
+        dft8(x0);
+        dft8(x1);
+        FFT_STAMP(16);
+        wave_lds_sync();
+#pragma unroll
+        for (int g1 = 0; g1 < 8; ++g1) { // b = lane + 64 gamma1
+            blk0[lane + 64 * g1] = x0[g1];
+            blk1[lane + 64 * g1] = x1[g1];
+        }
+    }
+    FFT_STAMP(17);
+    __syncthreads();
+    FFT_STAMP(18);
+
+    // ---- final: thread b = j gathers its 16 columns, * W_8192^(b c), 16-point DFT -> v[512 a + b]
+    double2 a[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) a[c] = flds[512 * c + j];
+    twiddle16(a, TWL(j));
+    dft16(a);
+    FFT_STAMP(19);
+
+    // ---- outputs: c[2m] = Re v'[m], c[2m+1] = -Im v'[m] (conj of the conj
+    // trick), m = 512 r + j, valid for c >= T-1.  Range-checked buffer over
+    // y[start, end): invalid lanes store to an out-of-range offset, which the
+    // hardware drops (no branches).
     float *yb = p.y + (int64_t)ch * p.y_stride + (p.start - p.y_lo);
     const __amdgpu_buffer_rsrc_t ys = __builtin_amdgcn_make_buffer_rsrc(
         yb, (short)0, (int)((p.end - p.start) * 4), 0x00020000);
@@ -343,13 +637,25 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     const int64_t off = n0 - cmin - p.start; // offset (samples) of c[0] from start
     const int64_t oend = p.end - p.start;
     float pk = 0.0f;
+    if (n0 - cmin + kFftL <= p.end) {
+        // every output of this unit is before `end`: the pair (c, c+1) is
+        // valid iff c >= cmin (cmin and o are even), so both stores share one
+        // offset and may merge into a dwordx2
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+        for (int r = 0; r < 16; ++r) {
+            const int c = 2 * (j + 512 * r);
+            const float f0 = (float)a[r].x, f1 = (float)(-a[r].y);
+            const bool ok = c >= cmin;
+            const int ob = ok ? (int)((off + c) * 4) : (int)0x80000000;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(f0), ys, ob, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(f1), ys, ob + 4, 0, 0);
+            pk = fmaxf(pk, ok ? fmaxf(fabsf(f0), fabsf(f1)) : 0.0f);
+        }
+    } else {
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const int c = 2 * (j + 512 * q + h * (kFftM / 2));
-            const double2 v = h ? hi[q] : lo[q];
-            const float f0 = (float)v.x, f1 = (float)(-v.y);
+        for (int r = 0; r < 16; ++r) {
+            const int c = 2 * (j + 512 * r);
+            const float f0 = (float)a[r].x, f1 = (float)(-a[r].y);
             const int64_t o = off + c;
             const bool ok0 = c >= cmin && o < oend, ok1 = c + 1 >= cmin && o + 1 < oend;
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(f0), ys,
@@ -359,14 +665,21 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
             pk = fmaxf(pk, fmaxf(ok0 ? fabsf(f0) : 0.0f, ok1 ? fabsf(f1) : 0.0f));
         }
     }
-    if (p.peak) {
-#pragma unroll
-        for (int s = 32; s >= 1; s >>= 1) pk = fmaxf(pk, __shfl_xor(pk, s, 64));
-        if ((j & 63) == 0) atomicMax(p.peak + ch * p.peak_stride, __float_as_uint(pk));
+    // fused peak: a running per-lane max, flushed (wave max + one atomic) only
+    // when this workgroup moves to another channel and at the end -- a
+    // per-unit atomic from every wave serialised on the peak slots and cost
+    // ~40 % of the kernel
+    if (ch != pk_ch) {
+        fft_peak_flush(p, pk_ch, pk_run);
+        pk_run = 0.0f;
+        pk_ch = ch;
     }
-    __syncthreads(); // the next unit's first LDS writes follow this unit's last reads
+    pk_run = fmaxf(pk_run, pk);
+    FFT_STAMP(20);
     }
+    fft_peak_flush(p, pk_ch, pk_run);
 }
+#undef TWL
 
 // ---------------------------------------------------------------------------
 // host side
@@ -404,6 +717,7 @@ inline void fft_ld(std::vector<long double> &re, std::vector<long double> &im) {
 }
 } // namespace detail
 
+
 inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, hipStream_t s,
                            std::string &err) {
     if (!fft_supported(ntaps)) {
@@ -420,23 +734,54 @@ inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, hipSt
     std::vector<long double> re((size_t)kFftL, 0.0L), im((size_t)kFftL, 0.0L);
     for (int i = 0; i < ntaps; ++i) re[(size_t)i] = (long double)taps[(size_t)(ntaps - 1 - i)];
     detail::fft_ld(re, im);
-    std::vector<double2> G((size_t)kFftM + 1);
     const long double scale = 1.0L / (4.0L * (long double)kFftM);
-    for (int k = 0; k <= kFftM; ++k)
-        G[(size_t)k] = make_double2((double)(re[(size_t)k] * scale), (double)(im[(size_t)k] * scale));
-    std::vector<double2> tw((size_t)kFftTwN);
     const long double two_pi = 6.283185307179586476925286766559L;
-    for (int i = 0; i < kFftTwN; ++i) {
-        const long double a = -two_pi * (long double)i / (long double)kFftL;
+    auto G = [&](int k) {
+        return make_double2((double)(re[(size_t)k] * scale), (double)(im[(size_t)k] * scale));
+    };
+    auto WL = [&](int k) {
+        const long double a = -two_pi * (long double)k / (long double)kFftL;
+        return make_double2((double)cosl(a), (double)sinl(a));
+    };
+    // pair table in consumption order: slot i of thread t holds bin k_i of
+    // its task A (special lane: the permuted list; slot 8: k = M/2)
+    std::vector<double2> pair((size_t)3 * kFftPairSlots * kFftNT);
+    std::vector<uint32_t> task((size_t)kFftNT);
+    for (int t = 0; t < kFftNT; ++t) {
+        const uint32_t tk = fft_task_word(t);
+        task[(size_t)t] = tk;
+        const int ca = tk & 15, da = (tk >> 4) & 7, ea = (tk >> 7) & 7;
+        const bool sp = t == kFftSpecialLane;
+        for (int i = 0; i < kFftPairSlots; ++i) {
+            int k;
+            if (i == 8) k = kFftM / 2;
+            else if (!sp) k = ca + 16 * (da + 8 * ea + 64 * i);
+            else k = i < 4 ? 512 + 1024 * i : (i < 7 ? 1024 * (i - 3) : 0);
+            const size_t o = (size_t)i * kFftNT + (size_t)t;
+            pair[o] = G(k);
+            pair[(size_t)kFftPairSlots * kFftNT + o] = G(kFftM - k);
+            pair[(size_t)2 * kFftPairSlots * kFftNT + o] = WL(k);
+        }
+    }
+    std::vector<double2> tw((size_t)kFftTw);
+    for (int i = 0; i < 512; ++i) {
+        const long double a = -two_pi * (long double)i / 8192.0L;
         tw[(size_t)i] = make_double2((double)cosl(a), (double)sinl(a));
     }
-    if (hipMalloc(reinterpret_cast<void **>(&plan.d_G), sizeof(double2) * G.size()) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void **>(&plan.d_tw), sizeof(double2) * tw.size()) != hipSuccess) {
+    for (int i = 0; i < 64; ++i) {
+        const long double a = -two_pi * (long double)i / 512.0L;
+        tw[(size_t)(512 + i)] = make_double2((double)cosl(a), (double)sinl(a));
+    }
+    if (hipMalloc(reinterpret_cast<void **>(&plan.d_pair), sizeof(double2) * pair.size()) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void **>(&plan.d_tw), sizeof(double2) * tw.size()) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void **>(&plan.d_task), sizeof(uint32_t) * task.size()) != hipSuccess) {
         err = "hipMalloc for the FFT plan failed";
         return false;
     }
-    if (hipMemcpy(plan.d_G, G.data(), sizeof(double2) * G.size(), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(plan.d_tw, tw.data(), sizeof(double2) * tw.size(), hipMemcpyHostToDevice) !=
+    if (hipMemcpy(plan.d_pair, pair.data(), sizeof(double2) * pair.size(), hipMemcpyHostToDevice) !=
+            hipSuccess ||
+        hipMemcpy(plan.d_tw, tw.data(), sizeof(double2) * tw.size(), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(plan.d_task, task.data(), sizeof(uint32_t) * task.size(), hipMemcpyHostToDevice) !=
             hipSuccess) {
         err = "FFT plan upload failed";
         return false;
@@ -453,9 +798,9 @@ inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, hipSt
     return true;
 }
 
-constexpr size_t fft_lds_bytes() { return sizeof(double2) * (size_t)(kFftM + kFftM / 16); }
+constexpr size_t fft_lds_bytes() { return sizeof(double2) * (size_t)(kFftM + kFftTw); }
 
-// workgroups per CU the persistent grid assumes (139 KiB of LDS each: one);
+// workgroups per CU the persistent grid assumes (137 KiB of LDS each: one);
 // LCFIR_FFT_BLOCKS_PER_CU overrides for experiments
 inline int fft_blocks_per_cu() {
     static const int v = [] {
@@ -484,7 +829,7 @@ inline bool fft_launch(const FftPlan &plan, const DirectParams &p, int nch, hipS
     const int64_t units = nseg * nch;
     const int64_t grid = std::min<int64_t>(units, (int64_t)plan.cus * fft_blocks_per_cu());
     hipLaunchKernelGGL(fir_fft_f64_kernel, dim3((unsigned)grid), dim3(kFftNT), fft_lds_bytes(), s,
-                       p, plan.d_G, plan.d_tw, plan.B, nseg, units);
+                       p, plan.d_pair, plan.d_tw, plan.d_task, plan.B, nseg, units);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         err = hipGetErrorString(e);
@@ -494,8 +839,9 @@ inline bool fft_launch(const FftPlan &plan, const DirectParams &p, int nch, hipS
 }
 
 inline void fft_plan_free(FftPlan &plan) {
-    if (plan.d_G) (void)hipFree(plan.d_G);
+    if (plan.d_pair) (void)hipFree(plan.d_pair);
     if (plan.d_tw) (void)hipFree(plan.d_tw);
+    if (plan.d_task) (void)hipFree(plan.d_task);
     plan = FftPlan{};
 }
 

@@ -101,6 +101,13 @@ def load(path: str = LIB_PATH):
         if not os.path.exists(path):
             raise LcfirError(EINTERNAL, f"{path} is missing: build it with "
                              "`python -c 'import __graft_entry__ as g; g.build()'`")
+        # torch first (when installed): its libamdhip64.so.7 then serves both,
+        # so device pointers from torch and from this library share one HIP
+        # runtime whatever order the caller imports them in (hip_runtimes()).
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         lib = ctypes.CDLL(path)
         for name, (argtypes, restype) in _SIGNATURES.items():
             fn = getattr(lib, name)

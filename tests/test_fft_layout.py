@@ -1,0 +1,71 @@
+"""CPU checks of the v3 FFT kernel's index plumbing (csrc/fir_fft.hpp):
+the wave-0 lane table and special lane in the header equal the ones
+scripts/fft_lds_sim.py derives, every LDS exchange is bank-conflict free under
+the gfx950 lane-group rules, and the kernel's full forward/inverse index flow
+(numpy) reproduces the 8192-point DFT with bins k and M-k in one lane."""
+import os
+import re
+import sys
+
+import numpy as np
+
+from conftest import ROOT
+
+sys.path.insert(0, os.path.join(ROOT, "scripts"))
+import fft_lds_sim as sim  # noqa: E402
+
+HDR = os.path.join(ROOT, "audio-fir-filter_amd", "csrc", "fir_fft.hpp")
+
+
+def _header():
+    return open(HDR).read()
+
+
+def test_header_tables_match_simulator():
+    s = _header()
+    body = re.search(r"kFftWave0C0\[32\] = \{([^}]*)\}", s).group(1)
+    words = [int(v, 16) for v in body.replace("\n", " ").split(",") if v.strip()]
+    want = []
+    for lane in range(32, 64):
+        (_, da, ea), (_, db, eb) = sim.WAVE0[lane]
+        want.append(da | ea << 3 | db << 6 | eb << 9)
+    assert words == want
+    special = int(re.search(r"kFftSpecialLane = (\d+);", s).group(1))
+    assert special == sim.SPECIAL_LANE
+
+
+def test_header_layouts_match_simulator():
+    s = _header()
+    # the C index functions, transcribed by regex into Python and compared
+    for name, f, n in [("fx1", lambda a, b: sim.x1(a, b), 2), ("fx2", sim.x2, 3),
+                       ("fx3", sim.x3, 3), ("fx4", sim.x4, 3)]:
+        m = re.search(name + r"\(([^)]*)\) \{\s*return ([^;]*);", s)
+        args = [a.split()[-1] for a in m.group(1).split(",")]
+        expr = m.group(2).replace("\n", " ")
+        g = eval("lambda " + ",".join(args) + ": " + expr)  # noqa: S307 - our own header
+        rng = range(64) if n == 2 else range(8)
+        for a in (range(64) if n == 2 else range(8)):
+            for b in range(8):
+                if n == 2:
+                    assert g(a, b) == f(a, b)
+                else:
+                    for c in range(8):
+                        assert g(a, b, c) == f(a, b, c)
+        del rng
+
+
+def test_exchanges_conflict_free():
+    rep = sim.check_banks()
+    assert all(v == 0 for v in rep.values()), rep
+
+
+def test_index_flow_is_the_dft():
+    rng = np.random.default_rng(7)
+    z = rng.standard_normal(sim.M) + 1j * rng.standard_normal(sim.M)
+    X, lanes = sim.forward_sim(z)
+    ref = np.fft.fft(z)
+    assert np.max(np.abs(X - ref)) <= 1e-12 * np.max(np.abs(ref))
+    for k in range(sim.M):
+        assert lanes[k][:2] == lanes[(sim.M - k) % sim.M][:2]
+    v = sim.inverse_sim(X)
+    assert np.max(np.abs(np.conj(v) - sim.M * np.conj(np.conj(z)))) <= 1e-9 * sim.M
