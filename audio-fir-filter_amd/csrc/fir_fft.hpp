@@ -141,6 +141,11 @@ __device__ __forceinline__ double2 cmul(double2 a, double2 b) {
 __device__ __forceinline__ double2 cmulc(double2 a, double2 b) {
     return make_double2(__builtin_fma(a.x, b.x, a.y * b.y), __builtin_fma(a.y, b.x, -(a.x * b.y)));
 }
+// per-component select: a ternary on a double2 can be lowered through scratch
+// memory (store both, load by a lane-dependent address)
+__device__ __forceinline__ double2 csel(bool c, double2 a, double2 b) {
+    return make_double2(c ? a.x : b.x, c ? a.y : b.y);
+}
 __device__ __forceinline__ double2 mul_mi(double2 a) { return make_double2(a.y, -a.x); } // * (-i)
 __device__ __forceinline__ double2 mul_pi(double2 a) { return make_double2(-a.y, a.x); } // * (+i)
 
@@ -490,17 +495,17 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
         if (w0) { // special lane: pairs (A_i, A_7-i), (B_1..3, B_7..5), (B_0, B_0)
             const double2 A[8] = {x0[0], x0[1], x0[2], x0[3], x0[4], x0[5], x0[6], x0[7]};
             const double2 Bv[8] = {x1[0], x1[1], x1[2], x1[3], x1[4], x1[5], x1[6], x1[7]};
-            x0[4] = sp ? Bv[1] : A[4];
-            x0[5] = sp ? Bv[2] : A[5];
-            x0[6] = sp ? Bv[3] : A[6];
-            x0[7] = sp ? Bv[0] : A[7];
-            x1[1] = sp ? Bv[5] : Bv[1];
-            x1[2] = sp ? Bv[6] : Bv[2];
-            x1[3] = sp ? Bv[7] : Bv[3];
-            x1[4] = sp ? A[4] : Bv[4];
-            x1[5] = sp ? A[5] : Bv[5];
-            x1[6] = sp ? A[6] : Bv[6];
-            x1[7] = sp ? A[7] : Bv[7];
+            x0[4] = csel(sp, Bv[1], A[4]);
+            x0[5] = csel(sp, Bv[2], A[5]);
+            x0[6] = csel(sp, Bv[3], A[6]);
+            x0[7] = csel(sp, Bv[0], A[7]);
+            x1[1] = csel(sp, Bv[5], Bv[1]);
+            x1[2] = csel(sp, Bv[6], Bv[2]);
+            x1[3] = csel(sp, Bv[7], Bv[3]);
+            x1[4] = csel(sp, A[4], Bv[4]);
+            x1[5] = csel(sp, A[5], Bv[5]);
+            x1[6] = csel(sp, A[6], Bv[6]);
+            x1[7] = csel(sp, A[7], Bv[7]);
         }
         // W_L^(k_i) = W_L^(k_0) W_16^i (k_i = k_0 + 1024 i); the special lane's
         // list (k = 512, 1536, 2560, 3584, 1024, 2048, 3072, 0) is patched in
@@ -519,7 +524,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
                 const double2 ws = i == 4 ? make_double2(kC1, -kS1)
                                  : i == 5 ? make_double2(kR2, -kR2)
                                  : i == 6 ? make_double2(kS1, -kC1) : make_double2(1.0, 0.0);
-                W = sp ? ws : W;
+                W = csel(sp, ws, W);
             }
             double2 Vk, Vmk;
             pair_step(x0[i], x1[7 - i], W, pg[i], pgm[i], Vk, Vmk);
@@ -531,18 +536,18 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
             pair_step(b4, b4, make_double2(0.0, -1.0), g4, g4, V4, Vx);
             const double2 A[8] = {x0[0], x0[1], x0[2], x0[3], x0[4], x0[5], x0[6], x0[7]};
             const double2 Bv[8] = {x1[0], x1[1], x1[2], x1[3], x1[4], x1[5], x1[6], x1[7]};
-            x0[4] = sp ? Bv[4] : A[4];
-            x0[5] = sp ? Bv[5] : A[5];
-            x0[6] = sp ? Bv[6] : A[6];
-            x0[7] = sp ? Bv[7] : A[7];
-            x1[0] = sp ? A[7] : Bv[0];
-            x1[1] = sp ? A[4] : Bv[1];
-            x1[2] = sp ? A[5] : Bv[2];
-            x1[3] = sp ? A[6] : Bv[3];
-            x1[4] = sp ? cconj(V4) : Bv[4];
-            x1[5] = sp ? Bv[1] : Bv[5];
-            x1[6] = sp ? Bv[2] : Bv[6];
-            x1[7] = sp ? Bv[3] : Bv[7];
+            x0[4] = csel(sp, Bv[4], A[4]);
+            x0[5] = csel(sp, Bv[5], A[5]);
+            x0[6] = csel(sp, Bv[6], A[6]);
+            x0[7] = csel(sp, Bv[7], A[7]);
+            x1[0] = csel(sp, A[7], Bv[0]);
+            x1[1] = csel(sp, A[4], Bv[1]);
+            x1[2] = csel(sp, A[5], Bv[2]);
+            x1[3] = csel(sp, A[6], Bv[3]);
+            x1[4] = csel(sp, cconj(V4), Bv[4]);
+            x1[5] = csel(sp, Bv[1], Bv[5]);
+            x1[6] = csel(sp, Bv[2], Bv[6]);
+            x1[7] = csel(sp, Bv[3], Bv[7]);
         }
     }
 
