@@ -61,15 +61,6 @@ __device__ unsigned long long g_fft_trace[64][8][24];
     } while (0)
 #endif
 
-#ifndef LCFIR_FFT_PREFETCH
-#define LCFIR_FFT_PREFETCH 1
-#endif
-#ifndef LCFIR_FFT_TWLDS
-#define LCFIR_FFT_TWLDS 1
-#endif
-#ifndef LCFIR_FFT_PAIRHOIST
-#define LCFIR_FFT_PAIRHOIST 1
-#endif
 
 namespace lcfir {
 
@@ -311,14 +302,11 @@ __device__ __forceinline__ void fft_load_unit(const DirectParams &p, int ch, int
     const int64_t w0 = n0 - p.half - p.x_lo; // window start inside the loaded range
     const int off0 = (int)(w0 * 4) + 8 * j;   // may be negative
     if (w0 >= 0 && w0 + kFftL <= p.x_hi - p.x_lo) {
-        // interior unit (all but the first and last of a range): plain cached
-        // loads, which the compiler may merge into dwordx2
+        // interior unit (all but the first and last of a range): cached
+        // dwordx2 loads (4-byte aligned is enough for buffer loads)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int off = off0 + 8 * 512 * r;
-            v[r].x = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, 0));
-            v[r].y = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, off + 4, 0, 0));
-        }
+        for (int r = 0; r < 16; ++r)
+            v[r] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rsrc, off0 + 8 * 512 * r, 0, 0));
     } else {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -344,25 +332,24 @@ __device__ __forceinline__ void fft_peak_flush(const DirectParams &p, int ch, fl
 // Persistent: one workgroup per CU walks the units u = blockIdx.x + i * gridDim.x
 // of the nch x nseg (channel, segment) grid.  The next unit's samples are
 // loaded during the current unit's inverse, so HBM latency is off the path.
+//
+// Inside a wave the two columns are software-pipelined through every
+// wave-local exchange: column 0's LDS writes are issued before column 1's
+// arithmetic, which then runs while the LDS drains them (sched_barrier pins
+// the order; the LDS executes one wave's operations in issue order, so each
+// read still follows the writes it needs).
 __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, const double2 *__restrict__ pair,
                                                             const double2 *__restrict__ tw,
                                                             const uint32_t *__restrict__ task, int B,
                                                             int64_t nseg, int64_t units) {
     extern __shared__ double2 flds[];
     double2 *twl = flds + kFftM; // the kFftTw twiddles, LDS-resident
-#if LCFIR_FFT_TWLDS
-#define TWL(i) twl[i]
     for (int i = threadIdx.x; i < kFftTw; i += kFftNT) twl[i] = tw[i];
-#else
-#define TWL(i) tw[i]
-#endif
     float2 v[16]; // samples of the unit about to start
-#if LCFIR_FFT_PREFETCH
     {
         const int64_t u = blockIdx.x;
         fft_load_unit(p, (int)(u / nseg), p.start + (u % nseg) * B, threadIdx.x, v);
     }
-#endif
     __syncthreads();
     float pk_run = 0.0f; // running max |y| of channel pk_ch over this lane's outputs
     int pk_ch = -1;
@@ -383,14 +370,11 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
 
     // ---- stage 1: thread b = j, 16-point DFT over z[512 a + b] -> column c
     {
-#if !LCFIR_FFT_PREFETCH
-        fft_load_unit(p, ch, n0, j, v);
-#endif
         double2 a[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) a[r] = make_double2((double)v[r].x, (double)v[r].y);
         dft16(a);
-        twiddle16(a, TWL(j)); // W_8192^(b c)
+        twiddle16(a, twl[j]); // W_8192^(b c)
         FFT_STAMP(1);
         __syncthreads();     // the previous unit's last reads are done
         FFT_STAMP(2);
@@ -405,48 +389,41 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     double2 tws[8];
     // ---- stage A: lane l holds b = l + 64 t; radix-8 over t -> d1; * W_512^(l d1)
 #pragma unroll
-    for (int t = 0; t < 8; ++t) {
-        x0[t] = blk0[lane + 64 * t];
-        x1[t] = blk1[lane + 64 * t];
-    }
-    dft8(x0);
-    dft8(x1);
-    powers8(TWL(512 + lane), tws);
-    twiddle8(x0, tws);
-    twiddle8(x1, tws);
-    FFT_STAMP(5);
-    wave_lds_sync();
+    for (int t = 0; t < 8; ++t) x0[t] = blk0[lane + 64 * t];
 #pragma unroll
-    for (int d1 = 0; d1 < 8; ++d1) {
-        blk0[fx1(lane, d1)] = x0[d1];
-        blk1[fx1(lane, d1)] = x1[d1];
-    }
+    for (int t = 0; t < 8; ++t) x1[t] = blk1[lane + 64 * t];
+    powers8(twl[512 + lane], tws);
+    dft8(x0);
+    twiddle8(x0, tws);
+#pragma unroll
+    for (int d1 = 0; d1 < 8; ++d1) blk0[fx1(lane, d1)] = x0[d1];
+    __builtin_amdgcn_sched_barrier(0);
+    dft8(x1);
+    twiddle8(x1, tws);
+#pragma unroll
+    for (int d1 = 0; d1 < 8; ++d1) blk1[fx1(lane, d1)] = x1[d1];
     wave_lds_sync();
-    FFT_STAMP(6);
+    FFT_STAMP(5);
     // ---- stage B: lane (l1, d1) gathers l2; radix-8 -> e1; * W_64^(l1 e1)
     {
         const int l1 = lane & 7, d1 = lane >> 3;
 #pragma unroll
-        for (int l2 = 0; l2 < 8; ++l2) {
-            x0[l2] = blk0[fx1(l1 + 8 * l2, d1)];
-            x1[l2] = blk1[fx1(l1 + 8 * l2, d1)];
-        }
-        dft8(x0);
-        dft8(x1);
-        powers8(TWL(512 + 8 * l1), tws);
-        twiddle8(x0, tws);
-        twiddle8(x1, tws);
-        FFT_STAMP(7);
-        wave_lds_sync();
+        for (int l2 = 0; l2 < 8; ++l2) x0[l2] = blk0[fx1(l1 + 8 * l2, d1)];
 #pragma unroll
-        for (int e1 = 0; e1 < 8; ++e1) {
-            blk0[fx2(l1, d1, e1)] = x0[e1];
-            blk1[fx2(l1, d1, e1)] = x1[e1];
-        }
+        for (int l2 = 0; l2 < 8; ++l2) x1[l2] = blk1[fx1(l1 + 8 * l2, d1)];
+        powers8(twl[512 + 8 * l1], tws);
+        dft8(x0);
+        twiddle8(x0, tws);
+#pragma unroll
+        for (int e1 = 0; e1 < 8; ++e1) blk0[fx2(l1, d1, e1)] = x0[e1];
+        __builtin_amdgcn_sched_barrier(0);
+        dft8(x1);
+        twiddle8(x1, tws);
+#pragma unroll
+        for (int e1 = 0; e1 < 8; ++e1) blk1[fx2(l1, d1, e1)] = x1[e1];
         wave_lds_sync();
-        FFT_STAMP(8);
     }
-#if LCFIR_FFT_PAIRHOIST
+    FFT_STAMP(6);
     // ---- pair-table loads, issued ahead of stage C (L2 latency off the path)
     double2 pg[8], pgm[8];
     const double2 g4 = pair[512 * 8 + j]; // G[M/2]: used by the special lane only
@@ -458,7 +435,6 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
             pgm[i] = t1[512 * i];
         }
     }
-#endif
     // ---- stage C: per task, radix-8 over l1 -> e2: x0[e2] = X[kA], x1[e2] = X[kB]
     const uint32_t tk = task[j];
     const int cA = tk & 15, dA = (tk >> 4) & 7, eA = (tk >> 7) & 7;
@@ -466,27 +442,13 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     {
         const double2 *ba = flds + 512 * cA, *bb = flds + 512 * cB;
 #pragma unroll
-        for (int l1 = 0; l1 < 8; ++l1) {
-            x0[l1] = ba[fx2(l1, dA, eA)];
-            x1[l1] = bb[fx2(l1, dB, eB)];
-        }
+        for (int l1 = 0; l1 < 8; ++l1) x0[l1] = ba[fx2(l1, dA, eA)];
+#pragma unroll
+        for (int l1 = 0; l1 < 8; ++l1) x1[l1] = bb[fx2(l1, dB, eB)];
     }
     dft8(x0);
     dft8(x1);
-    FFT_STAMP(9);
-#if !LCFIR_FFT_PAIRHOIST
-    // ---- pair-table loads, issued ahead of stage C (L2 latency off the path)
-    double2 pg[8], pgm[8];
-    const double2 g4 = pair[512 * 8 + j]; // G[M/2]: used by the special lane only
-    {
-        const double2 *t0 = pair + j, *t1 = pair + kFftPairSlots * 512 + j;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            pg[i] = t0[512 * i];
-            pgm[i] = t1[512 * i];
-        }
-    }
-#endif
+    FFT_STAMP(7);
     // ---- pair step in registers: pairs (x0[i], x1[7-i]); outputs conj(V)
     {
         const bool w0 = (w == 0); // wave-uniform
@@ -550,87 +512,77 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
             x1[7] = csel(sp, Bv[3], Bv[7]);
         }
     }
-
-    FFT_STAMP(10);
+    FFT_STAMP(8);
     // ---- prefetch the next unit's samples (consumed by its stage 1)
-    if (LCFIR_FFT_PREFETCH && u + gridDim.x < units) {
+    if (u + gridDim.x < units) {
         const int64_t un = u + gridDim.x;
         fft_load_unit(p, (int)(un / nseg), p.start + (un % nseg) * B, j, v);
     }
 
-    FFT_STAMP(11);
     // ---- inverse stage A': per task radix-8 over e2 -> beta0; * W_512^(beta0 d')
-    dft8(x0);
-    dft8(x1);
-    powers8(TWL(512 + dA + 8 * eA), tws);
-    twiddle8(x0, tws);
-    powers8(TWL(512 + dB + 8 * eB), tws);
-    twiddle8(x1, tws);
-    FFT_STAMP(12);
-    wave_lds_sync();
     {
         double2 *ba = flds + 512 * cA, *bb = flds + 512 * cB;
+        powers8(twl[512 + dA + 8 * eA], tws);
+        dft8(x0);
+        twiddle8(x0, tws);
 #pragma unroll
-        for (int b0 = 0; b0 < 8; ++b0) {
-            ba[fx3(dA, eA, b0)] = x0[b0];
-            bb[fx3(dB, eB, b0)] = x1[b0];
-        }
+        for (int b0 = 0; b0 < 8; ++b0) ba[fx3(dA, eA, b0)] = x0[b0];
+        __builtin_amdgcn_sched_barrier(0);
+        powers8(twl[512 + dB + 8 * eB], tws);
+        dft8(x1);
+        twiddle8(x1, tws);
+#pragma unroll
+        for (int b0 = 0; b0 < 8; ++b0) bb[fx3(dB, eB, b0)] = x1[b0];
     }
     wave_lds_sync();
-    FFT_STAMP(13);
+    FFT_STAMP(9);
     // ---- stage B': lane (d1, beta0) gathers e1; radix-8 -> gamma0; * W_64^(gamma0 d1)
+    // (wave 0's column-0 block was written by both tasks: both writes precede these reads)
     {
         const int d1 = lane & 7, b0 = lane >> 3;
 #pragma unroll
-        for (int e1 = 0; e1 < 8; ++e1) {
-            x0[e1] = blk0[fx3(d1, e1, b0)];
-            x1[e1] = blk1[fx3(d1, e1, b0)];
-        }
-        dft8(x0);
-        dft8(x1);
-        powers8(TWL(512 + 8 * d1), tws);
-        twiddle8(x0, tws);
-        twiddle8(x1, tws);
-        FFT_STAMP(14);
-        wave_lds_sync();
+        for (int e1 = 0; e1 < 8; ++e1) x0[e1] = blk0[fx3(d1, e1, b0)];
 #pragma unroll
-        for (int g0 = 0; g0 < 8; ++g0) {
-            blk0[fx4(d1, b0, g0)] = x0[g0];
-            blk1[fx4(d1, b0, g0)] = x1[g0];
-        }
+        for (int e1 = 0; e1 < 8; ++e1) x1[e1] = blk1[fx3(d1, e1, b0)];
+        powers8(twl[512 + 8 * d1], tws);
+        dft8(x0);
+        twiddle8(x0, tws);
+#pragma unroll
+        for (int g0 = 0; g0 < 8; ++g0) blk0[fx4(d1, b0, g0)] = x0[g0];
+        __builtin_amdgcn_sched_barrier(0);
+        dft8(x1);
+        twiddle8(x1, tws);
+#pragma unroll
+        for (int g0 = 0; g0 < 8; ++g0) blk1[fx4(d1, b0, g0)] = x1[g0];
         wave_lds_sync();
-        FFT_STAMP(15);
     }
+    FFT_STAMP(10);
     // ---- stage C': lane rho = beta0 + 8 gamma0 gathers d1; radix-8 -> gamma1
     {
         const int b0 = lane & 7, g0 = lane >> 3;
 #pragma unroll
-        for (int d1 = 0; d1 < 8; ++d1) {
-            x0[d1] = blk0[fx4(d1, b0, g0)];
-            x1[d1] = blk1[fx4(d1, b0, g0)];
-        }
-        dft8(x0);
-        dft8(x1);
-        FFT_STAMP(16);
-        wave_lds_sync();
+        for (int d1 = 0; d1 < 8; ++d1) x0[d1] = blk0[fx4(d1, b0, g0)];
 #pragma unroll
-        for (int g1 = 0; g1 < 8; ++g1) { // b = lane + 64 gamma1
-            blk0[lane + 64 * g1] = x0[g1];
-            blk1[lane + 64 * g1] = x1[g1];
-        }
+        for (int d1 = 0; d1 < 8; ++d1) x1[d1] = blk1[fx4(d1, b0, g0)];
+        dft8(x0);
+#pragma unroll
+        for (int g1 = 0; g1 < 8; ++g1) blk0[lane + 64 * g1] = x0[g1]; // b = lane + 64 gamma1
+        __builtin_amdgcn_sched_barrier(0);
+        dft8(x1);
+#pragma unroll
+        for (int g1 = 0; g1 < 8; ++g1) blk1[lane + 64 * g1] = x1[g1];
     }
-    FFT_STAMP(17);
+    FFT_STAMP(11);
     __syncthreads();
-    FFT_STAMP(18);
+    FFT_STAMP(12);
 
     // ---- final: thread b = j gathers its 16 columns, * W_8192^(b c), 16-point DFT -> v[512 a + b]
     double2 a[16];
 #pragma unroll
     for (int c = 0; c < 16; ++c) a[c] = flds[512 * c + j];
-    twiddle16(a, TWL(j));
+    twiddle16(a, twl[j]);
     dft16(a);
-    FFT_STAMP(19);
-
+    FFT_STAMP(13);
     // ---- outputs: c[2m] = Re v'[m], c[2m+1] = -Im v'[m] (conj of the conj
     // trick), m = 512 r + j, valid for c >= T-1.  Range-checked buffer over
     // y[start, end): invalid lanes store to an out-of-range offset, which the
@@ -680,11 +632,10 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
         pk_ch = ch;
     }
     pk_run = fmaxf(pk_run, pk);
-    FFT_STAMP(20);
+    FFT_STAMP(14);
     }
     fft_peak_flush(p, pk_ch, pk_run);
 }
-#undef TWL
 
 // ---------------------------------------------------------------------------
 // host side

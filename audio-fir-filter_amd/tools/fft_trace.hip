@@ -22,11 +22,12 @@
         }                                                                       \
     } while (0)
 
-static const char *kNames[] = {"stage1 load-wait+dft16", "B0 barrier",    "WG write",      "B1 barrier",
-                               "A: read+dft8+tw",        "x1 write",      "B: read+dft8+tw", "x2 write",
-                               "C: read+dft8",           "pair step",     "prefetch issue",  "A': dft8+tw",
-                               "x3 write",               "B': read+dft8+tw", "x4 write",     "C': read+dft8",
-                               "final write",            "B2 barrier",    "final read+tw+dft16", "stores+peak"};
+static const char *kNames[] = {"stage1 dft16+tw",    "B0 barrier",       "WG write",
+                               "B1 barrier",         "A + x1 exchange",  "B + x2 exchange",
+                               "C read+dft8",        "pair step",        "prefetch + A' + x3",
+                               "B' + x4 exchange",   "C' + final write", "B2 barrier",
+                               "final read+dft16",   "stores+peak"};
+constexpr int kPhases = 14;
 
 int main(int argc, char **argv) {
     const int64_t n = 28800000;
@@ -104,7 +105,7 @@ int main(int argc, char **argv) {
     for (int w = 0; w < 8; ++w) std::printf("%9d", w);
     std::printf("%9s\n", "avg");
     double total[8] = {0};
-    for (int ph = 0; ph < 20; ++ph) {
+    for (int ph = 0; ph < kPhases; ++ph) {
         std::printf("%-26s", kNames[ph]);
         double sum = 0;
         for (int w = 0; w < 8; ++w) {
