@@ -84,7 +84,7 @@ struct FftPlan {
     bool ready = false;
     int ntaps = 0;
     int B = 0;
-    double2 *d_pair = nullptr; // [3][kFftPairSlots][512]: G[k], G[M-k], W_L^k per (slot, thread)
+    double2 *d_pair = nullptr; // [3][kFftPairSlots][512]: 2S, 2D, W_L^k per (slot, thread)
     double2 *d_tw = nullptr;   // kFftTw twiddles
     uint32_t *d_task = nullptr; // [512] task words (cA, d1A, e1A, cB, d1B, e1B)
     int cus = 256;             // compute units of the plan's device (persistent grid)
@@ -270,25 +270,6 @@ __device__ __forceinline__ int fx4(int d1, int b0, int g0) {
     return 64 * g0 + 8 * b0 + (d1 ^ (((b0 >> 1) & 1) | ((g0 & 3) << 1)));
 }
 
-// Split/merge of the real transform fused with the filter multiply.
-// In: Zk = Z[k], Zmk = Z[M-k], W = W_L^k.  Out: V[k], V[M-k] (scaled by 4M,
-// folded into G).
-__device__ __forceinline__ void pair_step(double2 Zk, double2 Zmk, double2 W, double2 Gk,
-                                          double2 Gmk, double2 &Vk, double2 &Vmk) {
-    const double2 Zm = cconj(Zmk);
-    const double2 E = cadd(Zk, Zm);
-    const double2 O = mul_mi(csub(Zk, Zm));
-    const double2 WO = cmul(W, O);
-    const double2 Xk = cadd(E, WO);
-    const double2 Xmk = cconj(csub(E, WO));
-    const double2 Yk = cmul(Xk, Gk);
-    const double2 Ymk = cmul(Xmk, Gmk);
-    const double2 Ep = cadd(Yk, cconj(Ymk));
-    const double2 Op = cmulc(csub(Yk, cconj(Ymk)), W);
-    Vk = cadd(Ep, mul_pi(Op));
-    Vmk = cadd(cconj(Ep), mul_pi(cconj(Op)));
-}
-
 // Samples of one unit: v[r] = (x_seg[2m], x_seg[2m+1]), m = j + 512 r, x_seg[i] =
 // x[n0 - half + i].  Raw buffer loads through a range-checked resource over the
 // loaded window [x_lo, x_hi): offsets outside it -- including "negative" ones,
@@ -321,6 +302,75 @@ __device__ __forceinline__ void fft_load_unit(const DirectParams &p, int ch, int
     }
 }
 
+// W_L^(k_i) = W_L^(k_0) W_16^i for the pair in slot i (k_i = k_0 + 1024 i)
+__device__ __forceinline__ double2 fft_pair_w(double2 wbase, int i) {
+    switch (i) {
+    case 1: return cmul(wbase, make_double2(kC1, -kS1));
+    case 2: return w16<2>(wbase);
+    case 3: return cmul(wbase, make_double2(kS1, -kC1));
+    case 4: return mul_mi(wbase);
+    case 5: return cmul(wbase, make_double2(-kS1, -kC1));
+    case 6: return w16<6>(wbase);
+    case 7: return cmul(wbase, make_double2(-kC1, -kS1));
+    default: return wbase;
+    }
+}
+
+// One bin pair of the real split + filter multiply + merge (conj trick
+// applied): P = Z_k, Q = Z_{M-k}; S2 = 2S, D2 = 2D from the pair table.
+__device__ __forceinline__ void fft_pair(double2 P, double2 Q, double2 W, double2 S2, double2 D2,
+                                         double2 &oP, double2 &oQ) {
+    const double2 P1 = make_double2(__builtin_fma(D2.x, W.y, S2.x), __builtin_fma(D2.y, W.y, S2.y));
+    const double2 Q2 = make_double2(__builtin_fma(-D2.x, W.y, S2.x), __builtin_fma(-D2.y, W.y, S2.y));
+    const double2 P2 = make_double2(-D2.y * W.x, D2.x * W.x);
+    const double2 Zm = cconj(Q);
+    oP = cconj(cadd(cmul(P, P1), cmul(Zm, P2)));
+    oQ = csub(cmul(Zm, Q2), cmul(P, P2));
+}
+
+// Pair slot I of a wave-0 lane.  Generic lanes pair (x0[I], x1[7-I]); the
+// special lane pairs P = x0[I] (I < 4), x1[I-3] (I = 4..6), x1[0] (I = 7) with
+// Q = x0[7-I], x1[11-I], x1[0].  Operands are chosen by per-lane selects and
+// results written back in place (every register belongs to one pair in each
+// mapping), so nothing is copied.
+template <int I>
+__device__ __forceinline__ void fft_pair_w0(double2 (&x0)[8], double2 (&x1)[8], double2 wbase,
+                                            const double2 (&qs)[8], const double2 (&qd)[8], bool sp) {
+    double2 sP, sQ;
+    if constexpr (I < 4) {
+        sP = x0[I];
+        sQ = x0[7 - I];
+    } else if constexpr (I < 7) {
+        sP = x1[I - 3];
+        sQ = x1[11 - I];
+    } else {
+        sP = x1[0];
+        sQ = x1[0];
+    }
+    double2 W = fft_pair_w(wbase, I);
+    if constexpr (I >= 4) { // special lane: W_16^(I-3) for I < 7, 1 for I = 7
+        const double2 ws = I == 4 ? make_double2(kC1, -kS1)
+                         : I == 5 ? make_double2(kR2, -kR2)
+                         : I == 6 ? make_double2(kS1, -kC1) : make_double2(1.0, 0.0);
+        W = csel(sp, ws, W);
+    }
+    double2 oP, oQ;
+    fft_pair(csel(sp, sP, x0[I]), csel(sp, sQ, x1[7 - I]), W, qs[I], qd[I], oP, oQ);
+    if constexpr (I < 4) {
+        x0[I] = oP;                         // P register is the same in both mappings
+        x1[7 - I] = csel(sp, x1[7 - I], oQ);
+        x0[7 - I] = csel(sp, oQ, x0[7 - I]);
+    } else if constexpr (I < 7) {
+        x0[I] = csel(sp, x0[I], oP);
+        x1[7 - I] = csel(sp, x1[7 - I], oQ);
+        x1[I - 3] = csel(sp, oP, x1[I - 3]);
+        x1[11 - I] = csel(sp, oQ, x1[11 - I]);
+    } else { // k = 0 for the special lane: its V_k and V_{M-k} coincide
+        x0[7] = csel(sp, x0[7], oP);
+        x1[0] = oQ;
+    }
+}
+
 // Wave max of a running peak, one atomic per wave (channel ch < 0: nothing yet).
 __device__ __forceinline__ void fft_peak_flush(const DirectParams &p, int ch, float pk) {
     if (!p.peak || ch < 0) return;
@@ -331,7 +381,7 @@ __device__ __forceinline__ void fft_peak_flush(const DirectParams &p, int ch, fl
 
 // Persistent: one workgroup per CU walks the units u = blockIdx.x + i * gridDim.x
 // of the nch x nseg (channel, segment) grid.  The next unit's samples are
-// loaded during the current unit's inverse, so HBM latency is off the path.
+// loaded during the current unit's final phase, so HBM latency is off the path.
 //
 // Inside a wave the two columns are software-pipelined through every
 // wave-local exchange: column 0's LDS writes are issued before column 1's
@@ -425,14 +475,13 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     }
     FFT_STAMP(6);
     // ---- pair-table loads, issued ahead of stage C (L2 latency off the path)
-    double2 pg[8], pgm[8];
-    const double2 g4 = pair[512 * 8 + j]; // G[M/2]: used by the special lane only
+    double2 qs[8], qd[8]; // 2 S and 2 D of the pair in slot i
     {
-        const double2 *t0 = pair + j, *t1 = pair + kFftPairSlots * 512 + j;
+        const double2 *t = pair + j;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            pg[i] = t0[512 * i];
-            pgm[i] = t1[512 * i];
+            qs[i] = t[512 * i];
+            qd[i] = t[kFftPairSlots * 512 + 512 * i];
         }
     }
     // ---- stage C: per task, radix-8 over l1 -> e2: x0[e2] = X[kA], x1[e2] = X[kB]
@@ -449,73 +498,61 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     dft8(x0);
     dft8(x1);
     FFT_STAMP(7);
-    // ---- pair step in registers: pairs (x0[i], x1[7-i]); outputs conj(V)
+    // ---- pair step in registers: pairs (x0[i], x1[7-i]); outputs conj(V).
+    // The real split, the multiply by G and the merge collapse to
+    //   conj(V_k) = conj(Z_k P1 + conj(Z_{M-k}) P2),  conj(V_{M-k}) = conj(Z_{M-k}) Q2 - Z_k P2
+    // with S = G_k + conj(G_{M-k}), D = G_k - conj(G_{M-k}), W = W_L^k:
+    //   P1 = 2 (S + D Im W),  P2 = 2i D Re W,  Q2 = 2 (S - D Im W)
+    // The table holds 2S and 2D per (slot, thread) (host, long double); W comes
+    // from one per-thread base times W_16^i.
     {
-        const bool w0 = (w == 0); // wave-uniform
-        const bool sp = w0 && lane == kFftSpecialLane;
-        double2 b4 = x1[4];
-        if (w0) { // special lane: pairs (A_i, A_7-i), (B_1..3, B_7..5), (B_0, B_0)
-            const double2 A[8] = {x0[0], x0[1], x0[2], x0[3], x0[4], x0[5], x0[6], x0[7]};
-            const double2 Bv[8] = {x1[0], x1[1], x1[2], x1[3], x1[4], x1[5], x1[6], x1[7]};
-            x0[4] = csel(sp, Bv[1], A[4]);
-            x0[5] = csel(sp, Bv[2], A[5]);
-            x0[6] = csel(sp, Bv[3], A[6]);
-            x0[7] = csel(sp, Bv[0], A[7]);
-            x1[1] = csel(sp, Bv[5], Bv[1]);
-            x1[2] = csel(sp, Bv[6], Bv[2]);
-            x1[3] = csel(sp, Bv[7], Bv[3]);
-            x1[4] = csel(sp, A[4], Bv[4]);
-            x1[5] = csel(sp, A[5], Bv[5]);
-            x1[6] = csel(sp, A[6], Bv[6]);
-            x1[7] = csel(sp, A[7], Bv[7]);
-        }
-        // W_L^(k_i) = W_L^(k_0) W_16^i (k_i = k_0 + 1024 i); the special lane's
-        // list (k = 512, 1536, 2560, 3584, 1024, 2048, 3072, 0) is patched in
         const double2 wbase = pair[2 * kFftPairSlots * 512 + j];
+        // a scalar (wave-uniform) branch: a divergent one would keep both
+        // paths' copies of x0/x1 live
+        if (__builtin_amdgcn_readfirstlane(w) != 0) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            double2 W = wbase;
-            if (i == 1) W = cmul(wbase, make_double2(kC1, -kS1));
-            if (i == 2) W = w16<2>(wbase);
-            if (i == 3) W = cmul(wbase, make_double2(kS1, -kC1));
-            if (i == 4) W = mul_mi(wbase);
-            if (i == 5) W = cmul(wbase, make_double2(-kS1, -kC1));
-            if (i == 6) W = w16<6>(wbase);
-            if (i == 7) W = cmul(wbase, make_double2(-kC1, -kS1));
-            if (w0 && i >= 4) { // special lane: W_16^(i-3) for i < 7, 1 for i = 7
-                const double2 ws = i == 4 ? make_double2(kC1, -kS1)
-                                 : i == 5 ? make_double2(kR2, -kR2)
-                                 : i == 6 ? make_double2(kS1, -kC1) : make_double2(1.0, 0.0);
-                W = csel(sp, ws, W);
+            for (int i = 0; i < 8; ++i) {
+                fft_pair(x0[i], x1[7 - i], fft_pair_w(wbase, i), qs[i], qd[i], x0[i], x1[7 - i]);
+                __builtin_amdgcn_sched_barrier(0);
             }
-            double2 Vk, Vmk;
-            pair_step(x0[i], x1[7 - i], W, pg[i], pgm[i], Vk, Vmk);
-            x0[i] = cconj(Vk);
-            x1[7 - i] = cconj(Vmk);
-        }
-        if (w0) {
-            double2 V4, Vx;
-            pair_step(b4, b4, make_double2(0.0, -1.0), g4, g4, V4, Vx);
-            const double2 A[8] = {x0[0], x0[1], x0[2], x0[3], x0[4], x0[5], x0[6], x0[7]};
-            const double2 Bv[8] = {x1[0], x1[1], x1[2], x1[3], x1[4], x1[5], x1[6], x1[7]};
-            x0[4] = csel(sp, Bv[4], A[4]);
-            x0[5] = csel(sp, Bv[5], A[5]);
-            x0[6] = csel(sp, Bv[6], A[6]);
-            x0[7] = csel(sp, Bv[7], A[7]);
-            x1[0] = csel(sp, A[7], Bv[0]);
-            x1[1] = csel(sp, A[4], Bv[1]);
-            x1[2] = csel(sp, A[5], Bv[2]);
-            x1[3] = csel(sp, A[6], Bv[3]);
-            x1[4] = csel(sp, cconj(V4), Bv[4]);
-            x1[5] = csel(sp, Bv[1], Bv[5]);
-            x1[6] = csel(sp, Bv[2], Bv[6]);
-            x1[7] = csel(sp, Bv[3], Bv[7]);
+        } else {
+            // Wave 0: lane kFftSpecialLane holds the self-paired tasks (0,4) in
+            // A and (0,0) in B, whose pairs are (A_i, A_7-i), (B_1..3, B_7..5),
+            // (B_0, B_0) and (B_4, B_4) with k = 512 + 1024 i, 1024 (i - 3), 0,
+            // M/2 (the host's slot list).  Both mappings partition the 16
+            // registers into pairs, so operands are picked per pair by selects
+            // and results written back in place -- no register copies.
+            const bool sp = lane == kFftSpecialLane;
+            const double2 b4 = x1[4];
+            fft_pair_w0<0>(x0, x1, wbase, qs, qd, sp);
+            __builtin_amdgcn_sched_barrier(0);
+            fft_pair_w0<1>(x0, x1, wbase, qs, qd, sp);
+            __builtin_amdgcn_sched_barrier(0);
+            fft_pair_w0<2>(x0, x1, wbase, qs, qd, sp);
+            __builtin_amdgcn_sched_barrier(0);
+            fft_pair_w0<3>(x0, x1, wbase, qs, qd, sp);
+            __builtin_amdgcn_sched_barrier(0);
+            fft_pair_w0<4>(x0, x1, wbase, qs, qd, sp);
+            __builtin_amdgcn_sched_barrier(0);
+            fft_pair_w0<5>(x0, x1, wbase, qs, qd, sp);
+            __builtin_amdgcn_sched_barrier(0);
+            fft_pair_w0<6>(x0, x1, wbase, qs, qd, sp);
+            __builtin_amdgcn_sched_barrier(0);
+            fft_pair_w0<7>(x0, x1, wbase, qs, qd, sp);
+            __builtin_amdgcn_sched_barrier(0);
+            // bin M/2 of the special lane (slot 8, W = -i): P1 = S' - D', P2 = 0
+            const double2 V4c =
+                cconj(cmul(b4, csub(pair[512 * 8 + j], pair[kFftPairSlots * 512 + 512 * 8 + j])));
+            x1[4] = csel(sp, V4c, x1[4]);
         }
     }
+
     FFT_STAMP(8);
-    // ---- prefetch the next unit's samples (consumed by its stage 1)
-    if (u + gridDim.x < units) {
-        const int64_t un = u + gridDim.x;
+    // ---- prefetch the next unit's samples (consumed by its stage 1).
+    // Unconditional (the last unit reloads itself): a conditional load would
+    // keep the old v live across the whole loop body.
+    {
+        const int64_t un = u + gridDim.x < units ? u + gridDim.x : u;
         fft_load_unit(p, (int)(un / nseg), p.start + (un % nseg) * B, j, v);
     }
 
@@ -692,17 +729,13 @@ inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, hipSt
     detail::fft_ld(re, im);
     const long double scale = 1.0L / (4.0L * (long double)kFftM);
     const long double two_pi = 6.283185307179586476925286766559L;
-    auto G = [&](int k) {
-        return make_double2((double)(re[(size_t)k] * scale), (double)(im[(size_t)k] * scale));
-    };
-    auto WL = [&](int k) {
-        const long double a = -two_pi * (long double)k / (long double)kFftL;
-        return make_double2((double)cosl(a), (double)sinl(a));
-    };
     // pair table in consumption order: slot i of thread t holds bin k_i of
-    // its task A (special lane: the permuted list; slot 8: k = M/2)
+    // its task A (special lane: the permuted list; slot 8: k = M/2) as the
+    // collapsed split/multiply/merge coefficients 2S, 2D, plus W_L^k in the
+    // third field (the kernel reads slot 0's as its W base)
     std::vector<double2> pair((size_t)3 * kFftPairSlots * kFftNT);
     std::vector<uint32_t> task((size_t)kFftNT);
+    auto cplx = [](long double r, long double i) { return make_double2((double)r, (double)i); };
     for (int t = 0; t < kFftNT; ++t) {
         const uint32_t tk = fft_task_word(t);
         task[(size_t)t] = tk;
@@ -713,10 +746,16 @@ inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, hipSt
             if (i == 8) k = kFftM / 2;
             else if (!sp) k = ca + 16 * (da + 8 * ea + 64 * i);
             else k = i < 4 ? 512 + 1024 * i : (i < 7 ? 1024 * (i - 3) : 0);
+            const long double gr = re[(size_t)k] * scale, gi = im[(size_t)k] * scale;
+            const long double hr = re[(size_t)(kFftM - k)] * scale, hi = -im[(size_t)(kFftM - k)] * scale;
+            const long double sr = gr + hr, si = gi + hi; // S = G_k + conj(G_{M-k})
+            const long double dr = gr - hr, di = gi - hi; // D = G_k - conj(G_{M-k})
+            const long double a = -two_pi * (long double)k / (long double)kFftL;
+            const long double c = cosl(a), sn = sinl(a); // W = c + i sn
             const size_t o = (size_t)i * kFftNT + (size_t)t;
-            pair[o] = G(k);
-            pair[(size_t)kFftPairSlots * kFftNT + o] = G(kFftM - k);
-            pair[(size_t)2 * kFftPairSlots * kFftNT + o] = WL(k);
+            pair[o] = cplx(2 * sr, 2 * si);
+            pair[(size_t)kFftPairSlots * kFftNT + o] = cplx(2 * dr, 2 * di);
+            pair[(size_t)2 * kFftPairSlots * kFftNT + o] = cplx(c, sn);
         }
     }
     std::vector<double2> tw((size_t)kFftTw);

@@ -5,6 +5,7 @@
 //   hipcc -O3 --offload-arch=gfx950 -I../csrc -DLCFIR_FFT_TRACE fft_trace.hip -o fft_trace
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -83,16 +84,23 @@ int main(int argc, char **argv) {
     CK(hipEventCreate(&e1));
     for (int it = 0; it < 3; ++it)
         if (!lcfir::fft_launch(plan, p, nch, nullptr, err)) return 1;
-    CK(hipEventRecord(e0));
-    const int reps = 10;
-    for (int it = 0; it < reps; ++it)
-        if (!lcfir::fft_launch(plan, p, nch, nullptr, err)) return 1;
-    CK(hipEventRecord(e1));
-    CK(hipEventSynchronize(e1));
-    float ms = 0;
-    CK(hipEventElapsedTime(&ms, e0, e1));
+    // 5 rounds of 10 launches: min and median of the round means
+    const int reps = 10, rounds = 5;
+    std::vector<float> per;
+    for (int r = 0; r < rounds; ++r) {
+        CK(hipEventRecord(e0));
+        for (int it = 0; it < reps; ++it)
+            if (!lcfir::fft_launch(plan, p, nch, nullptr, err)) return 1;
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float t = 0;
+        CK(hipEventElapsedTime(&t, e0, e1));
+        per.push_back(t);
+    }
+    std::sort(per.begin(), per.end());
+    const float ms = per[rounds / 2], ms_min = per[0];
     const int64_t units = (int64_t)((n + plan.B - 1) / plan.B) * nch;
-    std::printf("kernel %.4f ms  (%.1f Gsamples/s), units %lld, units/WG %.2f\n", ms / reps,
+    std::printf("kernel %.4f ms (min %.4f)  (%.1f Gsamples/s), units %lld, units/WG %.2f\n", ms / reps, ms_min / reps,
                 (double)n * nch / (ms / reps * 1e-3) / 1e9, (long long)units, (double)units / plan.cus);
 #ifndef LCFIR_FFT_TRACE
     return 0;

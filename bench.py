@@ -39,8 +39,8 @@ METRIC = "filtered Msamples/sec @4001 taps; achieved HBM GB/s vs roofline"
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", type=int, default=2, choices=[2, 4, 5])
     ap.add_argument("--method", default="auto", choices=["auto", "direct", "fft"])
     ap.add_argument("--files", type=int, default=None, help="files in the batch (configs 4/5)")

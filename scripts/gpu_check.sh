@@ -19,10 +19,10 @@ step() { # name timeout cmd...
 }
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step pytest_gpu 1200 python -m pytest tests -m gpu -x -q
-step bench 600 python bench.py --steps 20 --warmup 3 "$@"
+step bench 600 python bench.py "$@"
 cd /tmp && export TMPDIR=/tmp
 step rocprof 600 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof_$TAG" -o bench -- \
-    python3 "$ROOT/bench.py" --steps 20 --warmup 3 --no-cpu-baseline --no-parity "$@"
+    python3 "$ROOT/bench.py" --no-cpu-baseline --no-parity "$@"
 cp "$OUT/prof_$TAG/bench_kernel_stats.csv" "$OUT/kernel_stats_$TAG.csv"
 for c in FETCH_SIZE WRITE_SIZE; do
     step "pmc_$c" 600 rocprofv3 --pmc $c --kernel-include-regex 'fir_' -f csv \
