@@ -26,7 +26,7 @@
 //           in registers (wave 0 needs one lane, kFftSpecialLane, permuted);
 //   the inverse runs the same stages in transposed order and ends with one
 //           workgroup-wide transpose and the 16-point DFTs.
-// Per segment: 3 workgroup barriers and 6 LDS round trips of the 128 KiB work
+// Per segment: 2 workgroup barriers and 6 LDS round trips of the 128 KiB work
 // array (the radix-16x16x16x2 Stockham form it replaces needed 14 barriers and
 // ~8 round trips).  The grid is persistent (one 512-thread workgroup per CU);
 // samples are read and results written through range-checked raw buffer
@@ -328,14 +328,14 @@ __device__ __forceinline__ void fft_pair(double2 P, double2 Q, double2 W, double
     oQ = csub(cmul(Zm, Q2), cmul(P, P2));
 }
 
-// Pair slot I of a wave-0 lane.  Generic lanes pair (x0[I], x1[7-I]); the
+// Pair slot I of a wave-0 lane (tq = the pair table at this thread).  Generic lanes pair (x0[I], x1[7-I]); the
 // special lane pairs P = x0[I] (I < 4), x1[I-3] (I = 4..6), x1[0] (I = 7) with
 // Q = x0[7-I], x1[11-I], x1[0].  Operands are chosen by per-lane selects and
 // results written back in place (every register belongs to one pair in each
 // mapping), so nothing is copied.
 template <int I>
 __device__ __forceinline__ void fft_pair_w0(double2 (&x0)[8], double2 (&x1)[8], double2 wbase,
-                                            const double2 (&qs)[8], const double2 (&qd)[8], bool sp) {
+                                            const double2 *tq, bool sp) {
     double2 sP, sQ;
     if constexpr (I < 4) {
         sP = x0[I];
@@ -355,7 +355,8 @@ __device__ __forceinline__ void fft_pair_w0(double2 (&x0)[8], double2 (&x1)[8], 
         W = csel(sp, ws, W);
     }
     double2 oP, oQ;
-    fft_pair(csel(sp, sP, x0[I]), csel(sp, sQ, x1[7 - I]), W, qs[I], qd[I], oP, oQ);
+    fft_pair(csel(sp, sP, x0[I]), csel(sp, sQ, x1[7 - I]), W, tq[512 * I], tq[kFftPairSlots * 512 + 512 * I],
+             oP, oQ);
     if constexpr (I < 4) {
         x0[I] = oP;                         // P register is the same in both mappings
         x1[7 - I] = csel(sp, x1[7 - I], oQ);
@@ -426,7 +427,9 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
         dft16(a);
         twiddle16(a, twl[j]); // W_8192^(b c)
         FFT_STAMP(1);
-        __syncthreads();     // the previous unit's last reads are done
+        // No barrier before this write: thread j overwrites exactly the
+        // addresses flds[512 c + j] it read itself in the previous unit's
+        // final phase, so program order already orders the two.
         FFT_STAMP(2);
 #pragma unroll
         for (int c = 0; c < 16; ++c) flds[512 * c + j] = a[c];
@@ -437,7 +440,11 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
 
     double2 x0[8], x1[8]; // the wave's two columns (later: tasks A and B)
     double2 tws[8];
+    // Stages A and B run as a two-column software pipeline: a column's
+    // exchange reads are issued right behind its writes, and the other
+    // column's arithmetic covers their latency (counted lgkmcnt waits).
     // ---- stage A: lane l holds b = l + 64 t; radix-8 over t -> d1; * W_512^(l d1)
+    const int l1 = lane & 7, d1s = lane >> 3; // the stage-B lane (l1, d1)
 #pragma unroll
     for (int t = 0; t < 8; ++t) x0[t] = blk0[lane + 64 * t];
 #pragma unroll
@@ -447,32 +454,31 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     twiddle8(x0, tws);
 #pragma unroll
     for (int d1 = 0; d1 < 8; ++d1) blk0[fx1(lane, d1)] = x0[d1];
+    wave_lds_sync();
+#pragma unroll
+    for (int l2 = 0; l2 < 8; ++l2) x0[l2] = blk0[fx1(l1 + 8 * l2, d1s)];
     __builtin_amdgcn_sched_barrier(0);
     dft8(x1);
     twiddle8(x1, tws);
 #pragma unroll
     for (int d1 = 0; d1 < 8; ++d1) blk1[fx1(lane, d1)] = x1[d1];
     wave_lds_sync();
+#pragma unroll
+    for (int l2 = 0; l2 < 8; ++l2) x1[l2] = blk1[fx1(l1 + 8 * l2, d1s)];
+    __builtin_amdgcn_sched_barrier(0);
     FFT_STAMP(5);
-    // ---- stage B: lane (l1, d1) gathers l2; radix-8 -> e1; * W_64^(l1 e1)
-    {
-        const int l1 = lane & 7, d1 = lane >> 3;
+    // ---- stage B: lane (l1, d1) has gathered l2; radix-8 -> e1; * W_64^(l1 e1)
+    powers8(twl[512 + 8 * l1], tws);
+    dft8(x0);
+    twiddle8(x0, tws);
 #pragma unroll
-        for (int l2 = 0; l2 < 8; ++l2) x0[l2] = blk0[fx1(l1 + 8 * l2, d1)];
+    for (int e1 = 0; e1 < 8; ++e1) blk0[fx2(l1, d1s, e1)] = x0[e1];
+    __builtin_amdgcn_sched_barrier(0);
+    dft8(x1);
+    twiddle8(x1, tws);
 #pragma unroll
-        for (int l2 = 0; l2 < 8; ++l2) x1[l2] = blk1[fx1(l1 + 8 * l2, d1)];
-        powers8(twl[512 + 8 * l1], tws);
-        dft8(x0);
-        twiddle8(x0, tws);
-#pragma unroll
-        for (int e1 = 0; e1 < 8; ++e1) blk0[fx2(l1, d1, e1)] = x0[e1];
-        __builtin_amdgcn_sched_barrier(0);
-        dft8(x1);
-        twiddle8(x1, tws);
-#pragma unroll
-        for (int e1 = 0; e1 < 8; ++e1) blk1[fx2(l1, d1, e1)] = x1[e1];
-        wave_lds_sync();
-    }
+    for (int e1 = 0; e1 < 8; ++e1) blk1[fx2(l1, d1s, e1)] = x1[e1];
+    wave_lds_sync();
     FFT_STAMP(6);
     // ---- pair-table loads, issued ahead of stage C (L2 latency off the path)
     double2 qs[8], qd[8]; // 2 S and 2 D of the pair in slot i
@@ -524,21 +530,21 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
             // and results written back in place -- no register copies.
             const bool sp = lane == kFftSpecialLane;
             const double2 b4 = x1[4];
-            fft_pair_w0<0>(x0, x1, wbase, qs, qd, sp);
+            fft_pair_w0<0>(x0, x1, wbase, pair + j, sp);
             __builtin_amdgcn_sched_barrier(0);
-            fft_pair_w0<1>(x0, x1, wbase, qs, qd, sp);
+            fft_pair_w0<1>(x0, x1, wbase, pair + j, sp);
             __builtin_amdgcn_sched_barrier(0);
-            fft_pair_w0<2>(x0, x1, wbase, qs, qd, sp);
+            fft_pair_w0<2>(x0, x1, wbase, pair + j, sp);
             __builtin_amdgcn_sched_barrier(0);
-            fft_pair_w0<3>(x0, x1, wbase, qs, qd, sp);
+            fft_pair_w0<3>(x0, x1, wbase, pair + j, sp);
             __builtin_amdgcn_sched_barrier(0);
-            fft_pair_w0<4>(x0, x1, wbase, qs, qd, sp);
+            fft_pair_w0<4>(x0, x1, wbase, pair + j, sp);
             __builtin_amdgcn_sched_barrier(0);
-            fft_pair_w0<5>(x0, x1, wbase, qs, qd, sp);
+            fft_pair_w0<5>(x0, x1, wbase, pair + j, sp);
             __builtin_amdgcn_sched_barrier(0);
-            fft_pair_w0<6>(x0, x1, wbase, qs, qd, sp);
+            fft_pair_w0<6>(x0, x1, wbase, pair + j, sp);
             __builtin_amdgcn_sched_barrier(0);
-            fft_pair_w0<7>(x0, x1, wbase, qs, qd, sp);
+            fft_pair_w0<7>(x0, x1, wbase, pair + j, sp);
             __builtin_amdgcn_sched_barrier(0);
             // bin M/2 of the special lane (slot 8, W = -i): P1 = S' - D', P2 = 0
             const double2 V4c =
@@ -574,9 +580,11 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     wave_lds_sync();
     FFT_STAMP(9);
     // ---- stage B': lane (d1, beta0) gathers e1; radix-8 -> gamma0; * W_64^(gamma0 d1)
-    // (wave 0's column-0 block was written by both tasks: both writes precede these reads)
+    // (wave 0's column-0 block was written by both tasks: both writes precede
+    // these reads).  B' and C' are software-pipelined like A and B.
     {
-        const int d1 = lane & 7, b0 = lane >> 3;
+        const int d1 = lane & 7, b0 = lane >> 3;  // stage-B' lane
+        const int rb0 = lane & 7, rg0 = lane >> 3; // stage-C' lane rho = beta0 + 8 gamma0
 #pragma unroll
         for (int e1 = 0; e1 < 8; ++e1) x0[e1] = blk0[fx3(d1, e1, b0)];
 #pragma unroll
@@ -586,29 +594,28 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
         twiddle8(x0, tws);
 #pragma unroll
         for (int g0 = 0; g0 < 8; ++g0) blk0[fx4(d1, b0, g0)] = x0[g0];
+        wave_lds_sync();
+#pragma unroll
+        for (int dd = 0; dd < 8; ++dd) x0[dd] = blk0[fx4(dd, rb0, rg0)];
         __builtin_amdgcn_sched_barrier(0);
         dft8(x1);
         twiddle8(x1, tws);
 #pragma unroll
         for (int g0 = 0; g0 < 8; ++g0) blk1[fx4(d1, b0, g0)] = x1[g0];
         wave_lds_sync();
+#pragma unroll
+        for (int dd = 0; dd < 8; ++dd) x1[dd] = blk1[fx4(dd, rb0, rg0)];
+        __builtin_amdgcn_sched_barrier(0);
     }
     FFT_STAMP(10);
-    // ---- stage C': lane rho = beta0 + 8 gamma0 gathers d1; radix-8 -> gamma1
-    {
-        const int b0 = lane & 7, g0 = lane >> 3;
+    // ---- stage C': lane rho = beta0 + 8 gamma0 has gathered d1; radix-8 -> gamma1
+    dft8(x0);
 #pragma unroll
-        for (int d1 = 0; d1 < 8; ++d1) x0[d1] = blk0[fx4(d1, b0, g0)];
+    for (int g1 = 0; g1 < 8; ++g1) blk0[lane + 64 * g1] = x0[g1]; // b = lane + 64 gamma1
+    __builtin_amdgcn_sched_barrier(0);
+    dft8(x1);
 #pragma unroll
-        for (int d1 = 0; d1 < 8; ++d1) x1[d1] = blk1[fx4(d1, b0, g0)];
-        dft8(x0);
-#pragma unroll
-        for (int g1 = 0; g1 < 8; ++g1) blk0[lane + 64 * g1] = x0[g1]; // b = lane + 64 gamma1
-        __builtin_amdgcn_sched_barrier(0);
-        dft8(x1);
-#pragma unroll
-        for (int g1 = 0; g1 < 8; ++g1) blk1[lane + 64 * g1] = x1[g1];
-    }
+    for (int g1 = 0; g1 < 8; ++g1) blk1[lane + 64 * g1] = x1[g1];
     FFT_STAMP(11);
     __syncthreads();
     FFT_STAMP(12);

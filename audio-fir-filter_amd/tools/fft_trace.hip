@@ -79,18 +79,19 @@ int main(int argc, char **argv) {
         p.peak = dpeak;
         p.peak_stride = 1;
     }
+    auto launch = [&]() { return lcfir::fft_launch(plan, p, nch, nullptr, err); };
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     for (int it = 0; it < 3; ++it)
-        if (!lcfir::fft_launch(plan, p, nch, nullptr, err)) return 1;
+        if (!launch()) return 1;
     // 5 rounds of 10 launches: min and median of the round means
     const int reps = 10, rounds = 5;
     std::vector<float> per;
     for (int r = 0; r < rounds; ++r) {
         CK(hipEventRecord(e0));
         for (int it = 0; it < reps; ++it)
-            if (!lcfir::fft_launch(plan, p, nch, nullptr, err)) return 1;
+            if (!launch()) return 1;
         CK(hipEventRecord(e1));
         CK(hipEventSynchronize(e1));
         float t = 0;

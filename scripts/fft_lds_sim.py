@@ -315,3 +315,199 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+# ---- v5: two workgroups per CU, 64 KiB work area, column-by-column rounds ----
+# LDS work area: 8 blocks x 512 entries of 16 B.  S(p, b) = block p entry b.
+# Strip of wave w: block t, entries 64 w .. 64 w + 63 (t = 0..7); in-wave
+# layouts index L in [0, 512) map to strip_addr(w, L) = 512 (L >> 6) + 64 w + (L & 63).
+def cols(w):
+    return (0, 8) if w == 0 else (w, 16 - w)
+
+
+def strip_addr(w, L):
+    return 512 * (L >> 6) + 64 * w + (L & 63)
+
+
+class LDS:
+    """Barrier-phased LDS model: a cross-wave hazard is any address written by
+    one wave and touched by another inside the same phase."""
+
+    def __init__(self):
+        self.mem = {}
+        self.new_phase()
+        self.hazards = 0
+
+    def new_phase(self):
+        self.writers, self.touch = {}, {}
+
+    def barrier(self):
+        self.new_phase()
+
+    def _note(self, w, a, write):
+        if write:
+            ow = self.writers.get(a)
+            if ow is not None and ow != w:
+                self.hazards += 1
+            for t in self.touch.get(a, ()):
+                if t != w:
+                    self.hazards += 1
+            self.writers[a] = w
+        else:
+            ow = self.writers.get(a)
+            if ow is not None and ow != w:
+                self.hazards += 1
+        self.touch.setdefault(a, set()).add(w)
+
+    def st(self, w, a, v):
+        assert 0 <= a < 4096
+        self._note(w, a, True)
+        self.mem[a] = v
+
+    def ld(self, w, a):
+        self._note(w, a, False)
+        return self.mem[a]
+
+
+def v5_forward(z, lds):
+    """Forward transform through the v5 LDS schedule; returns per-wave task
+    registers x0/x1 (as forward_sim's X) and checks against the DFT."""
+    # stage 1 (thread b): Y[b][c] after dft16 + twiddle
+    Y = np.zeros((512, 16), complex)
+    for b in range(512):
+        Y[b] = dft(z[b::512]) * W(M, b * np.arange(16))
+    # R1: thread b writes S(p, b) <- Y[b][c0(p)]
+    for b in range(512):
+        for p in range(8):
+            lds.st(b >> 6, 512 * p + b, Y[b][cols(p)[0]])
+    lds.barrier()
+    col = {}
+    for w in range(8):
+        col[(w, 0)] = np.array([lds.ld(w, 512 * w + bb) for bb in range(512)])  # lane l, t: b = l + 64 t
+    # R2: thread (w, l) writes block w entry l + 64 p <- Y[b][c1(p)]
+    for b in range(512):
+        w, l = b >> 6, b & 63
+        for p in range(8):
+            lds.st(w, 512 * w + l + 64 * p, Y[b][cols(p)[1]])
+    lds.barrier()
+    for p in range(8):
+        v = np.zeros(512, complex)
+        for t in range(8):
+            for l in range(64):
+                v[l + 64 * t] = lds.ld(p, 512 * t + l + 64 * p)
+        col[(p, 1)] = v
+    # in-wave stages per column, each exchange through the wave's strip
+    X = np.zeros(M, complex)
+    for w in range(8):
+        Q = {}
+        for s in (0, 1):
+            c = cols(w)[s]
+            Yc = col[(w, s)]
+            P = np.zeros((64, 8), complex)
+            for l in range(64):
+                P[l] = dft(Yc[l::64]) * W(512, l * np.arange(8))
+            for l in range(64):                      # exchange 1 (round s)
+                for d1 in range(8):
+                    lds.st(w, strip_addr(w, x1(l, d1)), P[l, d1])
+            R = np.zeros((64, 8), complex)
+            for lam in range(64):
+                l1, d1 = lam & 7, lam >> 3
+                v = np.array([lds.ld(w, strip_addr(w, x1(l1 + 8 * l2, d1))) for l2 in range(8)])
+                R[lam] = dft(v) * W(64, l1 * np.arange(8))
+            for lam in range(64):                    # exchange 2 write (round s)
+                l1, d1 = lam & 7, lam >> 3
+                for e1 in range(8):
+                    lds.st(w, strip_addr(w, x2(l1, d1, e1)), R[lam, e1])
+            # stage C reads of this round: lanes whose task lives in column c
+            for lane in range(64):
+                for which, (tc, d1, e1) in enumerate(tasks(w, lane)):
+                    if tc != c:
+                        continue
+                    v = np.array([lds.ld(w, strip_addr(w, x2(l1, d1, e1))) for l1 in range(8)])
+                    out = dft(v)
+                    for e2 in range(8):
+                        X[c + 16 * (d1 + 8 * e1 + 64 * e2)] = out[e2]
+    return X
+
+
+def v5_inverse(V, lds):
+    """Inverse through the v5 schedule (conj trick); returns v[512 a + b] before
+    the final conj."""
+    Vc = np.conj(V)
+    U = {}
+    for w in range(8):
+        for s in (0, 1):
+            c = cols(w)[s]
+            # x3 write (round s): tasks of this column, A' = dft8 over e2 + twiddle
+            for lane in range(64):
+                for (tc, d1, e1) in tasks(w, lane):
+                    if tc != c:
+                        continue
+                    dp = d1 + 8 * e1
+                    v = np.array([Vc[c + 16 * (dp + 64 * e2)] for e2 in range(8)])
+                    r = dft(v) * W(512, dp * np.arange(8))
+                    for b0 in range(8):
+                        lds.st(w, strip_addr(w, x3(d1, e1, b0)), r[b0])
+            S_ = np.zeros((64, 8), complex)
+            for nu in range(64):                     # B' (reads x3, writes x4)
+                d1, b0 = nu & 7, nu >> 3
+                v = np.array([lds.ld(w, strip_addr(w, x3(d1, e1, b0))) for e1 in range(8)])
+                S_[nu] = dft(v) * W(64, d1 * np.arange(8))
+            for nu in range(64):
+                d1, b0 = nu & 7, nu >> 3
+                for g0 in range(8):
+                    lds.st(w, strip_addr(w, x4(d1, b0, g0)), S_[nu, g0])
+            Uc = np.zeros(512, complex)
+            for rho in range(64):                    # C'
+                b0, g0 = rho & 7, rho >> 3
+                v = np.array([lds.ld(w, strip_addr(w, x4(d1, b0, g0))) for d1 in range(8)])
+                out = dft(v)
+                for g1 in range(8):
+                    b = rho + 64 * g1
+                    Uc[b] = out[g1] * W(M, b * c)
+            U[(w, s)] = Uc
+    # no barrier before final R1: every wave writes only its own strip
+    # final R1: wave w writes its strip: block g1, entry 64 w + rho <- col0 at b = rho + 64 g1
+    for w in range(8):
+        for b in range(512):
+            lds.st(w, 512 * (b >> 6) + 64 * w + (b & 63), U[(w, 0)][b])
+    lds.barrier()
+    A = np.zeros((512, 16), complex)
+    for b in range(512):
+        wp, l = b >> 6, b & 63
+        for p in range(8):
+            A[b][cols(p)[0]] = lds.ld(wp, 512 * wp + 64 * p + l)
+    # final R2: wave w writes S(w, b) <- col1 at b
+    for w in range(8):
+        for b in range(512):
+            lds.st(w, 512 * w + b, U[(w, 1)][b])
+    lds.barrier()
+    for b in range(512):
+        for p in range(8):
+            A[b][cols(p)[1]] = lds.ld(b >> 6, 512 * p + b)
+    v = np.zeros(M, complex)
+    for b in range(512):
+        v[b::512] = dft(A[b])
+    # the next unit's stage-1 R1 writes S(p, b) from thread b: the same
+    # addresses thread b just read (no WAR barrier) -- model it
+    for b in range(512):
+        for p in range(8):
+            lds.st(b >> 6, 512 * p + b, 0.0)
+    return v
+
+
+def check_v5():
+    """v5 data flow through the modelled LDS: forward and inverse relative
+    errors against numpy, and the count of cross-wave hazards inside barrier
+    phases (4 barriers per unit: after stage-1 R1 and R2 writes, after final
+    R1 and R2 writes)."""
+    rng = np.random.default_rng(11)
+    z = rng.standard_normal(M) + 1j * rng.standard_normal(M)
+    lds = LDS()
+    X = v5_forward(z, lds)
+    ref = np.fft.fft(z)
+    err_f = np.max(np.abs(X - ref)) / np.max(np.abs(ref))
+    # the forward's in-wave phase and the inverse's share one barrier phase
+    v = v5_inverse(X, lds)
+    err_i = np.max(np.abs(np.conj(v) - M * z)) / (M * np.max(np.abs(z)))
+    return err_f, err_i, lds.hazards
