@@ -160,11 +160,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("LCFIR_BENCH_SHARE_DEVICE") == "1":
+        # rehearsal of the multi-rank path on a box with fewer GPUs than ranks
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        if os.environ.get("LCFIR_BENCH_SHARE_DEVICE") == "1":
+            # RCCL refuses two ranks on one GPU: the rehearsal runs gloo
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
 
     import lcfir   # after torch: shares torch's HIP runtime (same SONAME)
     import synth
