@@ -813,13 +813,27 @@ inline int fft_blocks_per_cu() {
     return v;
 }
 
+// Outputs per launch.  The kernel addresses samples and outputs through raw
+// buffer resources with 32-bit byte offsets (and 0x80000000 as its "drop this
+// store" offset), so every launch's input window and output range must stay
+// well under 2 GiB: longer ranges are split into chunks, each with its own
+// narrowed input window.  Overlap-save is exact under any segmentation, and
+// an output only needs x[out - half, out + half], inside its chunk's window.
+// LCFIR_FFT_CHUNK overrides (tests exercise the chunk seams with small values).
+inline int64_t fft_chunk() {
+    static const int64_t v = [] {
+        const char *e = std::getenv("LCFIR_FFT_CHUNK");
+        const long long c = e ? std::atoll(e) : 0;
+        return c >= 4096 ? (int64_t)c : ((int64_t)1 << 28);
+    }();
+    return v;
+}
+
 inline bool fft_launch(const FftPlan &plan, const DirectParams &p, int nch, hipStream_t s,
                        std::string &err) {
-    const int64_t count = p.end - p.start;
-    if (count <= 0 || nch <= 0) return true;
-    const int64_t nseg = (count + plan.B - 1) / plan.B;
-    if (nseg > 0x7fffffff || nch > 65535) {
-        err = "range too large for one launch";
+    if (p.end - p.start <= 0 || nch <= 0) return true;
+    if (nch > 65535) {
+        err = "too many channels for one launch";
         return false;
     }
     static bool attr = [] {
@@ -828,14 +842,26 @@ inline bool fft_launch(const FftPlan &plan, const DirectParams &p, int nch, hipS
                                    (int)fft_lds_bytes()) == hipSuccess;
     }();
     (void)attr;
-    const int64_t units = nseg * nch;
-    const int64_t grid = std::min<int64_t>(units, (int64_t)plan.cus * fft_blocks_per_cu());
-    hipLaunchKernelGGL(fir_fft_f64_kernel, dim3((unsigned)grid), dim3(kFftNT), fft_lds_bytes(), s,
-                       p, plan.d_pair, plan.d_tw, plan.d_task, plan.B, nseg, units);
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) {
-        err = hipGetErrorString(e);
-        return false;
+    const int64_t chunk = fft_chunk();
+    for (int64_t cs = p.start; cs < p.end; cs += chunk) {
+        DirectParams q = p;
+        q.start = cs;
+        q.end = std::min(p.end, cs + chunk);
+        const int64_t lo = std::max(p.x_lo, q.start - p.half);
+        const int64_t hi = std::max(lo, std::min(p.x_hi, q.end + p.half));
+        q.x = p.x + (lo - p.x_lo);
+        q.x_lo = lo;
+        q.x_hi = hi;
+        const int64_t nseg = (q.end - q.start + plan.B - 1) / plan.B;
+        const int64_t units = nseg * nch;
+        const int64_t grid = std::min<int64_t>(units, (int64_t)plan.cus * fft_blocks_per_cu());
+        hipLaunchKernelGGL(fir_fft_f64_kernel, dim3((unsigned)grid), dim3(kFftNT), fft_lds_bytes(), s,
+                           q, plan.d_pair, plan.d_tw, plan.d_task, plan.B, nseg, units);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) {
+            err = hipGetErrorString(e);
+            return false;
+        }
     }
     return true;
 }

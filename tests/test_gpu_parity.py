@@ -282,3 +282,25 @@ def test_config3_full_size(lc, oracle_mod, method):
             ref_fma, _ = oracle_mod.filter_points(x[c], taps, idx, oracle_mod.MODE_FMA)
             assert np.array_equal(y[c][idx], ref_fma)
         assert pk[c] == np.abs(y[c]).max()
+
+
+@pytest.mark.slow
+def test_fft_channel_beyond_2gib(lc, oracle_mod):
+    """One channel of 2^29 + 4097 samples (2.15 GB of f32): past the 32-bit
+    byte range of the FFT kernel's buffer offsets, so fir_fft.hpp must split
+    the launch (fft_chunk, 2^28 outputs).  Checked against the long-double
+    oracle at both edges, around both chunk seams and at random positions;
+    the fused peak against the full output."""
+    n = (1 << 29) + 4097
+    rng = np.random.default_rng(29)
+    x = (rng.standard_normal(n, dtype=np.float32) * np.float32(0.2))[None, :]
+    taps = oracle_mod.design_lowcut(20.0, 48000.0, 4001)
+    flt = lc.Filter(taps, method="fft")
+    y, pk = gpu_filter_channels(lc, flt, x)
+    seams = np.r_[[(1 << 28) + d for d in range(-40, 40)], [(1 << 29) + d for d in range(-40, 40)]]
+    idx = np.unique(np.r_[_sample_positions(n, 2000, 2048, 29), seams])
+    ref_ld, _ = oracle_mod.filter_points(x[0], taps, idx, oracle_mod.MODE_LD)
+    assert rms(y[0][idx], ref_ld) <= RMS_TOL
+    assert max_ulps(y[0][idx], ref_ld) <= 1
+    assert pk[0] == np.abs(y[0]).max()
+    assert np.isfinite(y[0]).all()
