@@ -68,7 +68,8 @@ constexpr int kFftL = 16384;        // real segment length
 constexpr int kFftM = kFftL / 2;    // complex FFT length
 constexpr int kFftNT = 512;         // threads per workgroup
 constexpr int kFftMinB = 2048;      // smallest useful segment (B = L - T + 1)
-constexpr int kFftTw = 512 + 64;    // twiddles: W_8192^i (i < 512), W_512^i (i < 64)
+constexpr int kFftTw = 512 + 64 + 1; // LDS constants: W_8192^i (i < 512), W_512^i (i < 64), kFftC8
+constexpr int kFftC8 = 576;         // special lane's bin M/2 coefficient 2S - 2D
 constexpr int kFftPairSlots = 9;    // pair-table slots per thread (8 pairs + k = M/2)
 constexpr int kFftSpecialLane = 35; // wave-0 lane holding the self-paired bins 0 and M/2
 
@@ -328,48 +329,44 @@ __device__ __forceinline__ void fft_pair(double2 P, double2 Q, double2 W, double
     oQ = csub(cmul(Zm, Q2), cmul(P, P2));
 }
 
-// Pair slot I of a wave-0 lane (tq = the pair table at this thread).  Generic lanes pair (x0[I], x1[7-I]); the
-// special lane pairs P = x0[I] (I < 4), x1[I-3] (I = 4..6), x1[0] (I = 7) with
-// Q = x0[7-I], x1[11-I], x1[0].  Operands are chosen by per-lane selects and
-// results written back in place (every register belongs to one pair in each
-// mapping), so nothing is copied.
-template <int I>
-__device__ __forceinline__ void fft_pair_w0(double2 (&x0)[8], double2 (&x1)[8], double2 wbase,
-                                            const double2 *tq, bool sp) {
-    double2 sP, sQ;
-    if constexpr (I < 4) {
-        sP = x0[I];
-        sQ = x0[7 - I];
-    } else if constexpr (I < 7) {
-        sP = x1[I - 3];
-        sQ = x1[11 - I];
-    } else {
-        sP = x1[0];
-        sQ = x1[0];
-    }
-    double2 W = fft_pair_w(wbase, I);
-    if constexpr (I >= 4) { // special lane: W_16^(I-3) for I < 7, 1 for I = 7
-        const double2 ws = I == 4 ? make_double2(kC1, -kS1)
-                         : I == 5 ? make_double2(kR2, -kR2)
-                         : I == 6 ? make_double2(kS1, -kC1) : make_double2(1.0, 0.0);
-        W = csel(sp, ws, W);
-    }
-    double2 oP, oQ;
-    fft_pair(csel(sp, sP, x0[I]), csel(sp, sQ, x1[7 - I]), W, tq[512 * I], tq[kFftPairSlots * 512 + 512 * I],
-             oP, oQ);
-    if constexpr (I < 4) {
-        x0[I] = oP;                         // P register is the same in both mappings
-        x1[7 - I] = csel(sp, x1[7 - I], oQ);
-        x0[7 - I] = csel(sp, oQ, x0[7 - I]);
-    } else if constexpr (I < 7) {
-        x0[I] = csel(sp, x0[I], oP);
-        x1[7 - I] = csel(sp, x1[7 - I], oQ);
-        x1[I - 3] = csel(sp, oP, x1[I - 3]);
-        x1[11 - I] = csel(sp, oQ, x1[11 - I]);
-    } else { // k = 0 for the special lane: its V_k and V_{M-k} coincide
-        x0[7] = csel(sp, x0[7], oP);
-        x1[0] = oQ;
-    }
+// Wave 0's special lane (kFftSpecialLane) holds the self-paired tasks: A =
+// column-0 task (d1, e1) = (0, 4), bins 512 + 1024 e2, pairs (A_i, A_7-i); B =
+// task (0, 0), bins 1024 e2, pairs (B_i, B_8-i) with B_0 and B_4 self-paired.
+// Its registers are permuted (per-lane selects) into the generic layout
+// (P = x0[i], Q = x1[7-i]) so every lane runs the same pair loop:
+//   x0 = [A0 A1 A2 A3 B0 B1 B2 B3],  x1 = [B5 B6 B7 B0 A4 A5 A6 A7]
+// slots 0..3: k = 512 + 1024 i (W base W_L^512); slots 4..7: k = 1024 (i-4)
+// (W base +i = W_16^-4); B_4 (k = M/2) is done apart.  Each chain reads every
+// register before overwriting it, so no temporaries are needed.
+__device__ __forceinline__ void fft_w0_permute_in(double2 (&x0)[8], double2 (&x1)[8], bool sp) {
+    x1[4] = csel(sp, x0[4], x1[4]); // (B4 was taken out by the caller)
+    x0[4] = csel(sp, x1[0], x0[4]);
+    x1[0] = csel(sp, x1[5], x1[0]);
+    x1[5] = csel(sp, x0[5], x1[5]);
+    x0[5] = csel(sp, x1[1], x0[5]);
+    x1[1] = csel(sp, x1[6], x1[1]);
+    x1[6] = csel(sp, x0[6], x1[6]);
+    x0[6] = csel(sp, x1[2], x0[6]);
+    x1[2] = csel(sp, x1[7], x1[2]);
+    x1[7] = csel(sp, x0[7], x1[7]);
+    x0[7] = csel(sp, x1[3], x0[7]);
+    x1[3] = csel(sp, x0[4], x1[3]);
+}
+// Inverse of the above on the pair outputs (x1[3] holds a duplicate of B0's
+// output and is dropped); v4 = the output for B_4.
+__device__ __forceinline__ void fft_w0_permute_out(double2 (&x0)[8], double2 (&x1)[8], bool sp, double2 v4) {
+    x1[3] = csel(sp, x0[7], x1[3]);
+    x0[7] = csel(sp, x1[7], x0[7]);
+    x1[7] = csel(sp, x1[2], x1[7]);
+    x1[2] = csel(sp, x0[6], x1[2]);
+    x0[6] = csel(sp, x1[6], x0[6]);
+    x1[6] = csel(sp, x1[1], x1[6]);
+    x1[1] = csel(sp, x0[5], x1[1]);
+    x0[5] = csel(sp, x1[5], x0[5]);
+    x1[5] = csel(sp, x1[0], x1[5]);
+    x1[0] = csel(sp, x0[4], x1[0]);
+    x0[4] = csel(sp, x1[4], x0[4]);
+    x1[4] = csel(sp, v4, x1[4]);
 }
 
 // Wave max of a running peak, one atomic per wave (channel ch < 0: nothing yet).
@@ -513,44 +510,23 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     // from one per-thread base times W_16^i.
     {
         const double2 wbase = pair[2 * kFftPairSlots * 512 + j];
-        // a scalar (wave-uniform) branch: a divergent one would keep both
-        // paths' copies of x0/x1 live
-        if (__builtin_amdgcn_readfirstlane(w) != 0) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                fft_pair(x0[i], x1[7 - i], fft_pair_w(wbase, i), qs[i], qd[i], x0[i], x1[7 - i]);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        } else {
-            // Wave 0: lane kFftSpecialLane holds the self-paired tasks (0,4) in
-            // A and (0,0) in B, whose pairs are (A_i, A_7-i), (B_1..3, B_7..5),
-            // (B_0, B_0) and (B_4, B_4) with k = 512 + 1024 i, 1024 (i - 3), 0,
-            // M/2 (the host's slot list).  Both mappings partition the 16
-            // registers into pairs, so operands are picked per pair by selects
-            // and results written back in place -- no register copies.
-            const bool sp = lane == kFftSpecialLane;
-            const double2 b4 = x1[4];
-            fft_pair_w0<0>(x0, x1, wbase, pair + j, sp);
-            __builtin_amdgcn_sched_barrier(0);
-            fft_pair_w0<1>(x0, x1, wbase, pair + j, sp);
-            __builtin_amdgcn_sched_barrier(0);
-            fft_pair_w0<2>(x0, x1, wbase, pair + j, sp);
-            __builtin_amdgcn_sched_barrier(0);
-            fft_pair_w0<3>(x0, x1, wbase, pair + j, sp);
-            __builtin_amdgcn_sched_barrier(0);
-            fft_pair_w0<4>(x0, x1, wbase, pair + j, sp);
-            __builtin_amdgcn_sched_barrier(0);
-            fft_pair_w0<5>(x0, x1, wbase, pair + j, sp);
-            __builtin_amdgcn_sched_barrier(0);
-            fft_pair_w0<6>(x0, x1, wbase, pair + j, sp);
-            __builtin_amdgcn_sched_barrier(0);
-            fft_pair_w0<7>(x0, x1, wbase, pair + j, sp);
-            __builtin_amdgcn_sched_barrier(0);
-            // bin M/2 of the special lane (slot 8, W = -i): P1 = S' - D', P2 = 0
-            const double2 V4c =
-                cconj(cmul(b4, csub(pair[512 * 8 + j], pair[kFftPairSlots * 512 + 512 * 8 + j])));
-            x1[4] = csel(sp, V4c, x1[4]);
+        // Wave 0 (a scalar, wave-uniform branch) permutes its special lane
+        // into the generic layout first (fft_w0_permute_in).
+        const bool w0 = __builtin_amdgcn_readfirstlane(w) == 0;
+        const bool sp = w0 && lane == kFftSpecialLane;
+        double2 wb_hi = wbase; // W base of slots 4..7
+        double2 v4 = x1[4];    // special lane: B_4, bin M/2 (slot 8, W = -i): P1 = 2S - 2D, P2 = 0
+        if (w0) {
+            v4 = cconj(cmul(v4, twl[kFftC8])); // a plan constant in LDS (no L2 wait here)
+            wb_hi = csel(sp, make_double2(0.0, 1.0), wbase);
+            fft_w0_permute_in(x0, x1, sp);
         }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            fft_pair(x0[i], x1[7 - i], fft_pair_w(i < 4 ? wbase : wb_hi, i), qs[i], qd[i], x0[i], x1[7 - i]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (w0) fft_w0_permute_out(x0, x1, sp, v4);
     }
 
     FFT_STAMP(8);
@@ -752,7 +728,7 @@ inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, hipSt
             int k;
             if (i == 8) k = kFftM / 2;
             else if (!sp) k = ca + 16 * (da + 8 * ea + 64 * i);
-            else k = i < 4 ? 512 + 1024 * i : (i < 7 ? 1024 * (i - 3) : 0);
+            else k = i < 4 ? 512 + 1024 * i : 1024 * (i - 4); // fft_w0_permute_in
             const long double gr = re[(size_t)k] * scale, gi = im[(size_t)k] * scale;
             const long double hr = re[(size_t)(kFftM - k)] * scale, hi = -im[(size_t)(kFftM - k)] * scale;
             const long double sr = gr + hr, si = gi + hi; // S = G_k + conj(G_{M-k})
@@ -773,6 +749,11 @@ inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, hipSt
     for (int i = 0; i < 64; ++i) {
         const long double a = -two_pi * (long double)i / 512.0L;
         tw[(size_t)(512 + i)] = make_double2((double)cosl(a), (double)sinl(a));
+    }
+    {
+        const size_t o = (size_t)8 * kFftNT + kFftSpecialLane; // slot 8 of the special lane
+        const double2 s2 = pair[o], d2 = pair[(size_t)kFftPairSlots * kFftNT + o];
+        tw[kFftC8] = make_double2(s2.x - d2.x, s2.y - d2.y);
     }
     if (hipMalloc(reinterpret_cast<void **>(&plan.d_pair), sizeof(double2) * pair.size()) != hipSuccess ||
         hipMalloc(reinterpret_cast<void **>(&plan.d_tw), sizeof(double2) * tw.size()) != hipSuccess ||
