@@ -72,6 +72,7 @@ constexpr int kFftTw = 512 + 64 + 1; // LDS constants: W_8192^i (i < 512), W_512
 constexpr int kFftC8 = 576;         // special lane's bin M/2 coefficient 2S - 2D
 constexpr int kFftPairSlots = 9;    // pair-table slots per thread (8 pairs + k = M/2)
 constexpr int kFftSpecialLane = 35; // wave-0 lane holding the self-paired bins 0 and M/2
+constexpr int kVmcnt0 = 0x0F70;     // s_waitcnt vmcnt(0) (expcnt, lgkmcnt left at their maxima)
 
 // Wave 0, lanes 32..63: the column-0 task pairs (d1A | e1A << 3 | d1B << 6 |
 // e1B << 9), ordered so the exchange-2 reads and exchange-3 writes stay
@@ -398,7 +399,16 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
         const int64_t u = blockIdx.x;
         fft_load_unit(p, (int)(u / nseg), p.start + (u % nseg) * B, threadIdx.x, v);
     }
+    // vmcnt counts loads and stores together, in issue order, and the wait
+    // pass merges the loop's entry and back edge path-insensitively.  Both
+    // paths therefore reach the loop head with every prefetch load retired
+    // (here, and just before each unit's output stores), so stage 1 never
+    // waits on the previous unit's stores.
+    __builtin_amdgcn_s_waitcnt(kVmcnt0);
     __syncthreads();
+    // task word of this thread (exchange-2 tasks; fixed for the whole launch)
+    uint32_t tk_all = task[threadIdx.x];
+    asm volatile("" : "+v"(tk_all));
     float pk_run = 0.0f; // running max |y| of channel pk_ch over this lane's outputs
     int pk_ch = -1;
     for (int64_t u = blockIdx.x; u < units; u += gridDim.x) {
@@ -479,6 +489,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     FFT_STAMP(6);
     // ---- pair-table loads, issued ahead of stage C (L2 latency off the path)
     double2 qs[8], qd[8]; // 2 S and 2 D of the pair in slot i
+    const double2 wbase = pair[2 * kFftPairSlots * 512 + j]; // W_L^k of slot 0
     {
         const double2 *t = pair + j;
 #pragma unroll
@@ -487,8 +498,9 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
             qd[i] = t[kFftPairSlots * 512 + 512 * i];
         }
     }
+    __builtin_amdgcn_sched_barrier(0); // keep the loads ahead of stage C
     // ---- stage C: per task, radix-8 over l1 -> e2: x0[e2] = X[kA], x1[e2] = X[kB]
-    const uint32_t tk = task[j];
+    const uint32_t tk = tk_all;
     const int cA = tk & 15, dA = (tk >> 4) & 7, eA = (tk >> 7) & 7;
     const int cB = (tk >> 10) & 15, dB = (tk >> 14) & 7, eB = (tk >> 17) & 7;
     {
@@ -509,7 +521,6 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     // The table holds 2S and 2D per (slot, thread) (host, long double); W comes
     // from one per-thread base times W_16^i.
     {
-        const double2 wbase = pair[2 * kFftPairSlots * 512 + j];
         // Wave 0 (a scalar, wave-uniform branch) permutes its special lane
         // into the generic layout first (fft_w0_permute_in).
         const bool w0 = __builtin_amdgcn_readfirstlane(w) == 0;
@@ -607,6 +618,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     // trick), m = 512 r + j, valid for c >= T-1.  Range-checked buffer over
     // y[start, end): invalid lanes store to an out-of-range offset, which the
     // hardware drops (no branches).
+    __builtin_amdgcn_s_waitcnt(kVmcnt0); // the prefetch has landed long ago (see the loop head)
     float *yb = p.y + (int64_t)ch * p.y_stride + (p.start - p.y_lo);
     const __amdgpu_buffer_rsrc_t ys = __builtin_amdgcn_make_buffer_rsrc(
         yb, (short)0, (int)((p.end - p.start) * 4), 0x00020000);

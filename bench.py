@@ -33,6 +33,7 @@ sys.path.insert(0, os.path.join(ROOT, "audio-fir-filter_amd"))
 
 HBM_PEAK_GBPS = 8000.0      # MI355X_MICROARCH.md:36 (spec)
 FP64_PEAK_TFLOPS = 78.6     # FP64 vector (spec; half the 157.3 TF FP32 vector rate)
+VALU_NS_PER_INST = 2.0      # measured VALU issue ceiling per SIMD, two waves (tools/valu_rate.hip)
 METRIC = "filtered Msamples/sec @4001 taps; achieved HBM GB/s vs roofline"
 
 
@@ -247,15 +248,22 @@ def main():
             torch.cuda.synchronize(dev)
             rms, npos = parity_probe(x, y.cpu().numpy(), taps)
             del xd, y
-        traffic = None
+        traffic, f64_flops, valu_insts = None, None, None
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
             if tj.get("method") == method and tj.get("ntaps") == args.ntaps and \
                     tj.get("samples_per_launch") == samples_per_launch:
                 traffic = tj.get("hbm_bytes_per_launch")
+                f64_flops = tj.get("f64_flops_per_launch")
+                valu_insts = tj.get("valu_insts_per_launch")
         except (OSError, ValueError):
             pass
+        # The f64 kernels are bound by VALU issue, not HBM: the launch's PMC
+        # instruction counts (profiles/traffic_latest.json) over the live kernel time.
+        simds = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
+        fp64_tflops = f64_flops / kern_s / 1e12 if f64_flops else None
+        valu_frac = valu_insts * VALU_NS_PER_INST * 1e-9 / (simds * kern_s) if valu_insts else None
         wl = {2: "config2: 10 min stereo 48 kHz int24 file per GPU",
               4: f"config4: {nfiles} x {args.seconds / 60:g} min stereo 48 kHz int24 files",
               5: f"config5: {nfiles} x {args.seconds / 60:g} min stereo 48 kHz int24 files, "
@@ -295,7 +303,11 @@ def main():
                 "binding": "fp64-valu",
                 "direct_equiv_fp64_tflops": round(direct_tflops, 3),
                 "fp64_frac": round(direct_tflops / FP64_PEAK_TFLOPS, 4) if method == "direct"
-                else None,
+                else (round(fp64_tflops / FP64_PEAK_TFLOPS, 4) if fp64_tflops else None),
+                "fp64_tflops_pmc": round(fp64_tflops, 3) if fp64_tflops else None,
+                "valu_issue_frac": round(valu_frac, 4) if valu_frac else None,
+                "valu_issue_note": "PMC VALU wave-instructions per launch x 2.0 ns / (SIMDs x kernel time); "
+                                   "2.0 ns = measured two-wave issue ceiling (tools/valu_rate.hip)",
             },
             "parity": {"rms_vs_longdouble": rms, "positions": npos, "tol": 1e-9},
         }

@@ -1,6 +1,7 @@
 #!/bin/bash
 # GPU-box check: smoke -> pytest -m gpu -> bench -> rocprofv3 kernel stats ->
-# PMC HBM traffic (FETCH_SIZE / WRITE_SIZE, separate passes) -> traffic json.
+# PMC HBM traffic (FETCH_SIZE / WRITE_SIZE) and f64 VALU instruction counts,
+# each its own rocprofv3 --pmc pass -> pmc summary json.
 # Every GPU step has its own time limit; the first failure ends the script.
 # usage (from the repo root, on the GPU box): bash scripts/gpu_check.sh [tag] [bench args...]
 set -u -o pipefail
@@ -24,9 +25,11 @@ cd /tmp && export TMPDIR=/tmp
 step rocprof 600 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof_$TAG" -o bench -- \
     python3 "$ROOT/bench.py" --no-cpu-baseline --no-parity "$@"
 cp "$OUT/prof_$TAG/bench_kernel_stats.csv" "$OUT/kernel_stats_$TAG.csv"
-for c in FETCH_SIZE WRITE_SIZE; do
-    step "pmc_$c" 600 rocprofv3 --pmc $c --kernel-include-regex 'fir_' -f csv \
-        -d "$OUT/pmc_$TAG/p_$c" -o pmc -- \
+i=0
+for c in FETCH_SIZE WRITE_SIZE "SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64"; do
+    i=$((i+1))
+    step "pmc_$i" 600 rocprofv3 --pmc $c --kernel-include-regex 'fir_' -f csv \
+        -d "$OUT/pmc_$TAG/p_$i" -o pmc -- \
         python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-parity "$@"
 done
 cd "$ROOT"

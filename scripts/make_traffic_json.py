@@ -4,6 +4,9 @@ the per-launch HBM traffic bench.py reports as roofline.traffic.
 usage: python scripts/make_traffic_json.py <pmc_summary.json> <out.json> --method fft \
            --ntaps 4001 --samples-per-launch 57600000 --kernel fir_fft_f64_kernel
 
+Also carries the launch's VALU instruction count and f64 flops (SQ_INSTS_VALU*,
+when the summary has them) for bench.py's fp64 figures.
+
 HBM bytes per launch = 2 * FETCH_SIZE * 1024 (gfx950 FETCH_SIZE counts half the
 bytes of wide streaming reads: MI355X_MICROARCH.md, HBM section) + WRITE_SIZE * 1024.
 """
@@ -33,6 +36,11 @@ def main():
         "algorithmic_rw_bytes_per_launch": alg,
         "traffic_over_algorithmic": (read + write) / alg,
         "avg_duration_ns_profiled": k.get("avg_duration_ns"),
+        # f64 VALU work of one launch (wave instructions x 64 lanes; FMA = 2 flops)
+        "valu_insts_per_launch": k.get("SQ_INSTS_VALU"),
+        "f64_flops_per_launch": (64.0 * (k["SQ_INSTS_VALU_ADD_F64"] + k["SQ_INSTS_VALU_MUL_F64"]
+                                         + 2.0 * k["SQ_INSTS_VALU_FMA_F64"])
+                                 if "SQ_INSTS_VALU_FMA_F64" in k else None),
         "note": "FETCH_SIZE doubled per the gfx950 calibration; separate rocprofv3 --pmc passes",
     }
     json.dump(out, open(a.out, "w"), indent=1)
