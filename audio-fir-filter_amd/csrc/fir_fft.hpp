@@ -95,6 +95,14 @@ struct FftPlan {
 inline bool fft_supported(int ntaps) { return ntaps >= 1 && kFftL - ntaps + 1 >= kFftMinB; }
 inline bool fft_preferred(int ntaps) { return ntaps >= 96 && fft_supported(ntaps); }
 
+// LDS slot of column c: a wave's two columns sit in adjacent 8 KiB blocks
+// (w -> 2w, 16-w -> 2w+1; wave 0: 0 -> 0, 8 -> 1), so its second column's
+// exchange addresses are the first's plus an immediate offset.
+__host__ __device__ constexpr int fft_slot(int c) {
+    return c == 0 ? 0 : c == 8 ? 1 : c < 8 ? 2 * c : 33 - 2 * c;
+}
+constexpr int fft_slot_column(int s) { return s == 0 ? 0 : s == 1 ? 8 : s % 2 == 0 ? s / 2 : (33 - s) / 2; }
+
 // Task word of thread t = 64 w + lane after exchange 2: task A = (cA, d1A, e1A),
 // task B = (cB, d1B, e1B); bins k = c + 16 (d1 + 8 e1 + 64 e2), e2 = register.
 // Waves 1..7: columns w and 16 - w, B mirrors A, so X[k] (A[e2]) and X[M-k]
@@ -118,7 +126,8 @@ inline uint32_t fft_task_word(int t) {
         db = (v >> 6) & 7;
         eb = (v >> 9) & 7;
     }
-    return (uint32_t)(ca | da << 4 | ea << 7 | cb << 10 | db << 14 | eb << 17);
+    // the column fields hold LDS slots (fft_slot): the kernel only addresses with them
+    return (uint32_t)(fft_slot(ca) | da << 4 | ea << 7 | fft_slot(cb) << 10 | db << 14 | eb << 17);
 }
 
 // ---------------------------------------------------------------------------
@@ -418,10 +427,9 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     asm volatile("" : "+v"(j));
     const int lane = j & 63;
     const int w = j >> 6;
-    const int col0 = w == 0 ? 0 : w;        // the wave's two columns
-    const int col1 = w == 0 ? 8 : 16 - w;
-    double2 *blk0 = flds + 512 * col0;
-    double2 *blk1 = flds + 512 * col1;
+    // the wave's two columns {w, 16 - w} (wave 0: {0, 8}) in adjacent slots
+    double2 *blk0 = flds + 512 * (2 * w);
+    double2 *blk1 = blk0 + 512;
     const int ch = (int)(u / nseg);
     const int64_t n0 = p.start + (u % nseg) * B;
     FFT_STAMP(0);
@@ -439,7 +447,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
         // final phase, so program order already orders the two.
         FFT_STAMP(2);
 #pragma unroll
-        for (int c = 0; c < 16; ++c) flds[512 * c + j] = a[c];
+        for (int c = 0; c < 16; ++c) flds[512 * fft_slot(c) + j] = a[c];
         FFT_STAMP(3);
         __syncthreads();
         FFT_STAMP(4);
@@ -501,7 +509,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     __builtin_amdgcn_sched_barrier(0); // keep the loads ahead of stage C
     // ---- stage C: per task, radix-8 over l1 -> e2: x0[e2] = X[kA], x1[e2] = X[kB]
     const uint32_t tk = tk_all;
-    const int cA = tk & 15, dA = (tk >> 4) & 7, eA = (tk >> 7) & 7;
+    const int cA = tk & 15, dA = (tk >> 4) & 7, eA = (tk >> 7) & 7; // cA, cB: LDS slots
     const int cB = (tk >> 10) & 15, dB = (tk >> 14) & 7, eB = (tk >> 17) & 7;
     {
         const double2 *ba = flds + 512 * cA, *bb = flds + 512 * cB;
@@ -610,7 +618,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     // ---- final: thread b = j gathers its 16 columns, * W_8192^(b c), 16-point DFT -> v[512 a + b]
     double2 a[16];
 #pragma unroll
-    for (int c = 0; c < 16; ++c) a[c] = flds[512 * c + j];
+    for (int c = 0; c < 16; ++c) a[c] = flds[512 * fft_slot(c) + j];
     twiddle16(a, twl[j]);
     dft16(a);
     FFT_STAMP(13);
@@ -734,7 +742,7 @@ inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, hipSt
     for (int t = 0; t < kFftNT; ++t) {
         const uint32_t tk = fft_task_word(t);
         task[(size_t)t] = tk;
-        const int ca = tk & 15, da = (tk >> 4) & 7, ea = (tk >> 7) & 7;
+        const int ca = fft_slot_column(tk & 15), da = (tk >> 4) & 7, ea = (tk >> 7) & 7;
         const bool sp = t == kFftSpecialLane;
         for (int i = 0; i < kFftPairSlots; ++i) {
             int k;
