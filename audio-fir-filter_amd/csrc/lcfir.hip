@@ -417,8 +417,12 @@ int lcfir_filter_window_dev(lcfir_ctx *ctx, const float *d_xw, int64_t x_lo, int
 
 int lcfir_peak_reset_dev(float *d_peak, int32_t count, void *stream) {
     if (!d_peak || count < 0) return fail(LCFIR_EINVAL, "bad peak buffer");
-    LCFIR_HIP(hipMemsetAsync(d_peak, 0, sizeof(float) * (size_t)count,
-                             reinterpret_cast<hipStream_t>(stream)));
+    if (count == 0) return LCFIR_OK;
+    // one small block (the runtime's fill kernel for a hipMemsetAsync of a few
+    // bytes costs ~2x as long on the stream)
+    hipLaunchKernelGGL(lcfir::peak_zero_kernel, dim3(1), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), peak_bits(d_peak), count);
+    LCFIR_HIP(hipGetLastError());
     return LCFIR_OK;
 }
 
@@ -440,7 +444,9 @@ int lcfir_normalize_dev(float *d_y, int64_t stride, int32_t nch, int64_t n, cons
         return fail(LCFIR_EINVAL, "bad argument");
     if (nch == 0 || n == 0) return LCFIR_OK;
     if (nch > 65535) return fail(LCFIR_EINVAL, "too many channels");
-    const int blocks = stream_blocks(n, 256 * 16);
+    // grid-stride: 256 blocks per channel already saturate HBM when the pass
+    // rescales, and keep the (common) no-op launch short
+    const int blocks = std::min(stream_blocks(n, 256 * 16), 256);
     hipLaunchKernelGGL(lcfir::normalize_kernel, dim3(blocks, nch), dim3(256), 0,
                        reinterpret_cast<hipStream_t>(stream), d_y, stride, n,
                        reinterpret_cast<const unsigned *>(d_peak), npeak, force);

@@ -41,6 +41,10 @@ __global__ __launch_bounds__(256) void peak_kernel(const float *__restrict__ y, 
     if ((threadIdx.x & 63) == 0) atomicMax(peak + blockIdx.y, __float_as_uint(m));
 }
 
+__global__ __launch_bounds__(256) void peak_zero_kernel(unsigned *__restrict__ peak, int count) {
+    for (int i = threadIdx.x; i < count; i += blockDim.x) peak[i] = 0u;
+}
+
 __device__ __forceinline__ float scale_one(float v, double gain) {
     return (float)((double)v * gain);
 }
