@@ -45,6 +45,8 @@ struct DirectParams {
     int32_t tc;         // taps per LDS stage (multiple of 2R)
     unsigned *peak;     // max|y| as float bits (nullable): channel c -> peak[c * peak_stride]
     int64_t peak_stride;
+    double *y64;        // partitioned FFT only: f64 partial sums, element 0 = output `start`
+    int64_t y64_stride;
 };
 
 template <int R>

@@ -68,11 +68,13 @@ constexpr int kFftL = 16384;        // real segment length
 constexpr int kFftM = kFftL / 2;    // complex FFT length
 constexpr int kFftNT = 512;         // threads per workgroup
 constexpr int kFftMinB = 2048;      // smallest useful segment (B = L - T + 1)
-constexpr int kFftTw = 512 + 64 + 1; // LDS constants: W_8192^i (i < 512), W_512^i (i < 64), kFftC8
-constexpr int kFftC8 = 576;         // special lane's bin M/2 coefficient 2S - 2D
+constexpr int kFftTw = 512 + 64;    // LDS twiddles: W_8192^i (i < 512), W_512^i (i < 64)
+constexpr int kFftMaxPartTaps = kFftL - kFftMinB + 1; // longest partition (14 337 taps)
 constexpr int kFftPairSlots = 9;    // pair-table slots per thread (8 pairs + k = M/2)
 constexpr int kFftSpecialLane = 35; // wave-0 lane holding the self-paired bins 0 and M/2
 constexpr int kVmcnt0 = 0x0F70;     // s_waitcnt vmcnt(0) (expcnt, lgkmcnt left at their maxima)
+// output modes of fir_fft_f64_kernel (see there)
+constexpr int kFftOutF32 = 0, kFftOutFirst = 1, kFftOutAdd = 2, kFftOutLast = 3;
 
 // Wave 0, lanes 32..63: the column-0 task pairs (d1A | e1A << 3 | d1B << 6 |
 // e1B << 9), ordered so the exchange-2 reads and exchange-3 writes stay
@@ -82,18 +84,50 @@ constexpr uint16_t kFftWave0C0[32] = {
     0xd0c, 0x373, 0x3f1, 0xc10, 0x5aa, 0xb92, 0x91c, 0xe86, 0xad5, 0xa18, 0x95b,
     0x5e9, 0x46f, 0xf82, 0xe08, 0x8dd, 0x2b6, 0xf04, 0xd4b, 0x9d9, 0x277};
 
+constexpr int kFftMaxTaps = 1 << 20; // longest filter (partitions of <= kFftMaxPartTaps)
+constexpr size_t kFftPairTable = (size_t)3 * kFftPairSlots * kFftNT; // double2 per pair table
+
+// A filter longer than one segment allows is split into `parts` equal
+// partitions of `ntaps` taps (odd, zero padded at the end), each convolved by
+// its own launch with the input offset half - p * ntaps; the launches sum in
+// f64 (fir_fft_f64_kernel's output modes).
 struct FftPlan {
     bool ready = false;
-    int ntaps = 0;
-    int B = 0;
-    double2 *d_pair = nullptr; // [3][kFftPairSlots][512]: 2S, 2D, W_L^k per (slot, thread)
+    int ntaps = 0;             // taps per partition (the filter's own count when parts == 1)
+    int parts = 1;
+    int B = 0;                 // outputs per segment = L - ntaps + 1
+    double2 *d_pair = nullptr; // parts x [3][kFftPairSlots][512]: 2S, 2D, W_L^k per (slot, thread)
+    std::vector<double2> c8;   // per partition: the special lane's bin-M/2 coefficient
     double2 *d_tw = nullptr;   // kFftTw twiddles
     uint32_t *d_task = nullptr; // [512] task words (cA, d1A, e1A, cB, d1B, e1B)
     int cus = 256;             // compute units of the plan's device (persistent grid)
 };
 
-inline bool fft_supported(int ntaps) { return ntaps >= 1 && kFftL - ntaps + 1 >= kFftMinB; }
+inline bool fft_supported(int ntaps) { return ntaps >= 1 && ntaps <= kFftMaxTaps; }
 inline bool fft_preferred(int ntaps) { return ntaps >= 96 && fft_supported(ntaps); }
+
+// taps per partition when `parts` partitions share `ntaps` taps (odd: the
+// kernel's output pairing assumes an even T - 1)
+inline int fft_partition_taps(int ntaps, int parts) {
+    const int t = (ntaps + parts - 1) / parts;
+    return t | 1;
+}
+// partition count minimising the work per output, parts / (L - taps + 1)
+inline int fft_partition_count(int ntaps) {
+    int best = 0;
+    double best_cost = 0.0;
+    for (int n = 1; n <= ntaps; ++n) {
+        const int t = fft_partition_taps(ntaps, n);
+        if (t > kFftMaxPartTaps) continue;
+        const double cost = (double)n / (double)(kFftL - t + 1);
+        if (best == 0 || cost < best_cost) {
+            best = n;
+            best_cost = cost;
+        }
+        if (t < kFftL / 4) break; // more partitions only add launches from here
+    }
+    return best;
+}
 
 // LDS slot of column c: a wave's two columns sit in adjacent 8 KiB blocks
 // (w -> 2w, 16-w -> 2w+1; wave 0: 0 -> 0, 8 -> 1), so its second column's
@@ -396,10 +430,19 @@ __device__ __forceinline__ void fft_peak_flush(const DirectParams &p, int ch, fl
 // arithmetic, which then runs while the LDS drains them (sched_barrier pins
 // the order; the LDS executes one wave's operations in issue order, so each
 // read still follows the writes it needs).
+//
+// kOut selects what a unit does with its outputs (filters longer than one
+// partition run one launch per partition over the same range, fft_launch):
+//   kFftOutF32   : RNE to f32 into y, fused peak (single-partition filters);
+//   kFftOutFirst : write the f64 partial sum into the scratch p.y64;
+//   kFftOutAdd   : add it to p.y64;
+//   kFftOutLast  : RNE(p.y64 + partial) to f32 into y, fused peak.
+// c8 = the special lane's bin-M/2 coefficient 2S - 2D of this pair table.
+template <int kOut>
 __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, const double2 *__restrict__ pair,
                                                             const double2 *__restrict__ tw,
                                                             const uint32_t *__restrict__ task, int B,
-                                                            int64_t nseg, int64_t units) {
+                                                            int64_t nseg, int64_t units, double2 c8) {
     extern __shared__ double2 flds[];
     double2 *twl = flds + kFftM; // the kFftTw twiddles, LDS-resident
     for (int i = threadIdx.x; i < kFftTw; i += kFftNT) twl[i] = tw[i];
@@ -536,7 +579,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
         double2 wb_hi = wbase; // W base of slots 4..7
         double2 v4 = x1[4];    // special lane: B_4, bin M/2 (slot 8, W = -i): P1 = 2S - 2D, P2 = 0
         if (w0) {
-            v4 = cconj(cmul(v4, twl[kFftC8])); // a plan constant in LDS (no L2 wait here)
+            v4 = cconj(cmul(v4, c8)); // a kernel argument (SGPRs: no L2 wait here)
             wb_hi = csel(sp, make_double2(0.0, 1.0), wbase);
             fft_w0_permute_in(x0, x1, sp);
         }
@@ -634,6 +677,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     const int64_t off = n0 - cmin - p.start; // offset (samples) of c[0] from start
     const int64_t oend = p.end - p.start;
     float pk = 0.0f;
+    if constexpr (kOut == kFftOutF32) {
     if (n0 - cmin + kFftL <= p.end) {
         // every output of this unit is before `end`: the pair (c, c+1) is
         // valid iff c >= cmin (cmin and o are even), so both stores share one
@@ -660,6 +704,41 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(f1), ys,
                                                   ok1 ? (int)(o * 4 + 4) : (int)0x80000000, 0, 0);
             pk = fmaxf(pk, fmaxf(ok0 ? fabsf(f0) : 0.0f, ok1 ? fabsf(f1) : 0.0f));
+        }
+    }
+    } else {
+        // partitioned filter: the f64 partial sums of outputs [start, end) live
+        // in the scratch p.y64 (element 0 = output `start`, channel stride
+        // y64_stride); every output belongs to exactly one unit per launch, so
+        // the read-modify-write needs no atomics.  Invalid outputs use an
+        // out-of-range offset: their loads return 0 and their stores drop.
+        double *zb = p.y64 + (int64_t)ch * p.y64_stride;
+        const __amdgpu_buffer_rsrc_t zs = __builtin_amdgcn_make_buffer_rsrc(
+            zb, (short)0, (int)(oend * 8), 0x00020000);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int c = 2 * (j + 512 * r);
+            const int64_t o = off + c;
+            const bool ok0 = c >= cmin && o < oend, ok1 = c + 1 >= cmin && o + 1 < oend;
+            const int oz0 = ok0 ? (int)(o * 8) : (int)0x80000000;
+            const int oz1 = ok1 ? (int)(o * 8 + 8) : (int)0x80000000;
+            double v0 = a[r].x, v1 = -a[r].y;
+            if constexpr (kOut != kFftOutFirst) {
+                v0 += __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(zs, oz0, 0, 0));
+                v1 += __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(zs, oz1, 0, 0));
+            }
+            if constexpr (kOut == kFftOutLast) {
+                const float f0 = (float)v0, f1 = (float)v1;
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(f0), ys,
+                                                      ok0 ? (int)(o * 4) : (int)0x80000000, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(f1), ys,
+                                                      ok1 ? (int)(o * 4 + 4) : (int)0x80000000, 0, 0);
+                pk = fmaxf(pk, fmaxf(ok0 ? fabsf(f0) : 0.0f, ok1 ? fabsf(f1) : 0.0f));
+            } else {
+                using b64_t = decltype(__builtin_amdgcn_raw_buffer_load_b64(zs, 0, 0, 0));
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(b64_t, v0), zs, oz0, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(b64_t, v1), zs, oz1, 0, 0);
+            }
         }
     }
     // fused peak: a running per-lane max, flushed (wave max + one atomic) only
@@ -717,7 +796,7 @@ inline void fft_ld(std::vector<long double> &re, std::vector<long double> &im) {
 inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, hipStream_t s,
                            std::string &err) {
     if (!fft_supported(ntaps)) {
-        err = "tap count too large for the L=16384 overlap-save segment";
+        err = "tap count outside the FFT method's range";
         return false;
     }
     std::vector<double> taps((size_t)ntaps);
@@ -726,40 +805,55 @@ inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, hipSt
         err = "tap download failed";
         return false;
     }
-    // G = FFT_L(g), g[j] = h[T-1-j], zero padded; scaled by 1/(4M)
-    std::vector<long double> re((size_t)kFftL, 0.0L), im((size_t)kFftL, 0.0L);
-    for (int i = 0; i < ntaps; ++i) re[(size_t)i] = (long double)taps[(size_t)(ntaps - 1 - i)];
-    detail::fft_ld(re, im);
+    const int parts = fft_partition_count(ntaps);
+    const int tp = parts == 1 ? ntaps : fft_partition_taps(ntaps, parts);
     const long double scale = 1.0L / (4.0L * (long double)kFftM);
     const long double two_pi = 6.283185307179586476925286766559L;
-    // pair table in consumption order: slot i of thread t holds bin k_i of
+    // pair tables in consumption order: slot i of thread t holds bin k_i of
     // its task A (special lane: the permuted list; slot 8: k = M/2) as the
     // collapsed split/multiply/merge coefficients 2S, 2D, plus W_L^k in the
     // third field (the kernel reads slot 0's as its W base)
-    std::vector<double2> pair((size_t)3 * kFftPairSlots * kFftNT);
+    std::vector<double2> pair((size_t)parts * kFftPairTable);
     std::vector<uint32_t> task((size_t)kFftNT);
+    std::vector<double2> c8((size_t)parts);
     auto cplx = [](long double r, long double i) { return make_double2((double)r, (double)i); };
-    for (int t = 0; t < kFftNT; ++t) {
-        const uint32_t tk = fft_task_word(t);
-        task[(size_t)t] = tk;
-        const int ca = fft_slot_column(tk & 15), da = (tk >> 4) & 7, ea = (tk >> 7) & 7;
-        const bool sp = t == kFftSpecialLane;
-        for (int i = 0; i < kFftPairSlots; ++i) {
-            int k;
-            if (i == 8) k = kFftM / 2;
-            else if (!sp) k = ca + 16 * (da + 8 * ea + 64 * i);
-            else k = i < 4 ? 512 + 1024 * i : 1024 * (i - 4); // fft_w0_permute_in
-            const long double gr = re[(size_t)k] * scale, gi = im[(size_t)k] * scale;
-            const long double hr = re[(size_t)(kFftM - k)] * scale, hi = -im[(size_t)(kFftM - k)] * scale;
-            const long double sr = gr + hr, si = gi + hi; // S = G_k + conj(G_{M-k})
-            const long double dr = gr - hr, di = gi - hi; // D = G_k - conj(G_{M-k})
-            const long double a = -two_pi * (long double)k / (long double)kFftL;
-            const long double c = cosl(a), sn = sinl(a); // W = c + i sn
-            const size_t o = (size_t)i * kFftNT + (size_t)t;
-            pair[o] = cplx(2 * sr, 2 * si);
-            pair[(size_t)kFftPairSlots * kFftNT + o] = cplx(2 * dr, 2 * di);
-            pair[(size_t)2 * kFftPairSlots * kFftNT + o] = cplx(c, sn);
+    std::vector<long double> re((size_t)kFftL), im((size_t)kFftL);
+    for (int part = 0; part < parts; ++part) {
+        // G = FFT_L(g), g[j] = h_p[tp-1-j] with h_p[k] = h[part * tp + k] (0 past
+        // the filter's end), zero padded; scaled by 1/(4M)
+        std::fill(re.begin(), re.end(), 0.0L);
+        std::fill(im.begin(), im.end(), 0.0L);
+        for (int i = 0; i < tp; ++i) {
+            const int64_t k = (int64_t)part * tp + (tp - 1 - i);
+            re[(size_t)i] = k < ntaps ? (long double)taps[(size_t)k] : 0.0L;
         }
+        detail::fft_ld(re, im);
+        double2 *pt = pair.data() + (size_t)part * kFftPairTable;
+        for (int t = 0; t < kFftNT; ++t) {
+            const uint32_t tk = fft_task_word(t);
+            task[(size_t)t] = tk;
+            const int ca = fft_slot_column(tk & 15), da = (tk >> 4) & 7, ea = (tk >> 7) & 7;
+            const bool sp = t == kFftSpecialLane;
+            for (int i = 0; i < kFftPairSlots; ++i) {
+                int k;
+                if (i == 8) k = kFftM / 2;
+                else if (!sp) k = ca + 16 * (da + 8 * ea + 64 * i);
+                else k = i < 4 ? 512 + 1024 * i : 1024 * (i - 4); // fft_w0_permute_in
+                const long double gr = re[(size_t)k] * scale, gi = im[(size_t)k] * scale;
+                const long double hr = re[(size_t)(kFftM - k)] * scale, hi = -im[(size_t)(kFftM - k)] * scale;
+                const long double sr = gr + hr, si = gi + hi; // S = G_k + conj(G_{M-k})
+                const long double dr = gr - hr, di = gi - hi; // D = G_k - conj(G_{M-k})
+                const long double a = -two_pi * (long double)k / (long double)kFftL;
+                const long double c = cosl(a), sn = sinl(a); // W = c + i sn
+                const size_t o = (size_t)i * kFftNT + (size_t)t;
+                pt[o] = cplx(2 * sr, 2 * si);
+                pt[(size_t)kFftPairSlots * kFftNT + o] = cplx(2 * dr, 2 * di);
+                pt[(size_t)2 * kFftPairSlots * kFftNT + o] = cplx(c, sn);
+            }
+        }
+        const size_t o = (size_t)8 * kFftNT + kFftSpecialLane; // slot 8 of the special lane
+        const double2 s2 = pt[o], d2 = pt[(size_t)kFftPairSlots * kFftNT + o];
+        c8[(size_t)part] = make_double2(s2.x - d2.x, s2.y - d2.y);
     }
     std::vector<double2> tw((size_t)kFftTw);
     for (int i = 0; i < 512; ++i) {
@@ -769,11 +863,6 @@ inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, hipSt
     for (int i = 0; i < 64; ++i) {
         const long double a = -two_pi * (long double)i / 512.0L;
         tw[(size_t)(512 + i)] = make_double2((double)cosl(a), (double)sinl(a));
-    }
-    {
-        const size_t o = (size_t)8 * kFftNT + kFftSpecialLane; // slot 8 of the special lane
-        const double2 s2 = pair[o], d2 = pair[(size_t)kFftPairSlots * kFftNT + o];
-        tw[kFftC8] = make_double2(s2.x - d2.x, s2.y - d2.y);
     }
     if (hipMalloc(reinterpret_cast<void **>(&plan.d_pair), sizeof(double2) * pair.size()) != hipSuccess ||
         hipMalloc(reinterpret_cast<void **>(&plan.d_tw), sizeof(double2) * tw.size()) != hipSuccess ||
@@ -795,8 +884,10 @@ inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, hipSt
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
         cus > 0)
         plan.cus = cus;
-    plan.ntaps = ntaps;
-    plan.B = kFftL - ntaps + 1;
+    plan.ntaps = tp;
+    plan.parts = parts;
+    plan.B = kFftL - tp + 1;
+    plan.c8 = std::move(c8);
     plan.ready = true;
     return true;
 }
@@ -830,6 +921,31 @@ inline int64_t fft_chunk() {
     return v;
 }
 
+template <int kOut>
+inline bool fft_launch_one(const FftPlan &plan, const DirectParams &q, int part, int nch, hipStream_t s,
+                           std::string &err) {
+    static const bool attr = [] {
+        return hipFuncSetAttribute(reinterpret_cast<const void *>(&fir_fft_f64_kernel<kOut>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)fft_lds_bytes()) == hipSuccess;
+    }();
+    (void)attr;
+    const int64_t nseg = (q.end - q.start + plan.B - 1) / plan.B;
+    const int64_t units = nseg * nch;
+    const int64_t grid = std::min<int64_t>(units, (int64_t)plan.cus * fft_blocks_per_cu());
+    hipLaunchKernelGGL(fir_fft_f64_kernel<kOut>, dim3((unsigned)grid), dim3(kFftNT), fft_lds_bytes(), s, q,
+                       plan.d_pair + (size_t)part * kFftPairTable, plan.d_tw, plan.d_task, plan.B, nseg,
+                       units, plan.c8[(size_t)part]);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        err = hipGetErrorString(e);
+        return false;
+    }
+    return true;
+}
+
+// Filter outputs [p.start, p.end) of nch channels.  p.half / p.ntaps are the
+// filter's own (the plan holds the partitioning).
 inline bool fft_launch(const FftPlan &plan, const DirectParams &p, int nch, hipStream_t s,
                        std::string &err) {
     if (p.end - p.start <= 0 || nch <= 0) return true;
@@ -837,30 +953,46 @@ inline bool fft_launch(const FftPlan &plan, const DirectParams &p, int nch, hipS
         err = "too many channels for one launch";
         return false;
     }
-    static bool attr = [] {
-        return hipFuncSetAttribute(reinterpret_cast<const void *>(&fir_fft_f64_kernel),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)fft_lds_bytes()) == hipSuccess;
-    }();
-    (void)attr;
-    const int64_t chunk = fft_chunk();
+    // partitioned filters keep f64 partial sums: 2^26 outputs keep the
+    // scratch's byte offsets inside the 32-bit buffer range
+    const int64_t chunk = plan.parts == 1 ? fft_chunk() : std::min<int64_t>(fft_chunk(), (int64_t)1 << 26);
     for (int64_t cs = p.start; cs < p.end; cs += chunk) {
         DirectParams q = p;
         q.start = cs;
         q.end = std::min(p.end, cs + chunk);
+        // every partition reads inside x[start - half, end - half + T - 1)
         const int64_t lo = std::max(p.x_lo, q.start - p.half);
-        const int64_t hi = std::max(lo, std::min(p.x_hi, q.end + p.half));
+        const int64_t hi = std::max(lo, std::min(p.x_hi, q.end - p.half + p.ntaps - 1));
         q.x = p.x + (lo - p.x_lo);
         q.x_lo = lo;
         q.x_hi = hi;
-        const int64_t nseg = (q.end - q.start + plan.B - 1) / plan.B;
-        const int64_t units = nseg * nch;
-        const int64_t grid = std::min<int64_t>(units, (int64_t)plan.cus * fft_blocks_per_cu());
-        hipLaunchKernelGGL(fir_fft_f64_kernel, dim3((unsigned)grid), dim3(kFftNT), fft_lds_bytes(), s,
-                           q, plan.d_pair, plan.d_tw, plan.d_task, plan.B, nseg, units);
-        const hipError_t e = hipGetLastError();
+        q.ntaps = plan.ntaps;
+        if (plan.parts == 1) {
+            if (!fft_launch_one<kFftOutF32>(plan, q, 0, nch, s, err)) return false;
+            continue;
+        }
+        const int64_t count = q.end - q.start;
+        double *z = nullptr;
+        hipError_t e = hipMallocAsync(reinterpret_cast<void **>(&z), sizeof(double) * (size_t)(count * nch), s);
         if (e != hipSuccess) {
-            err = hipGetErrorString(e);
+            err = std::string("partial-sum scratch: ") + hipGetErrorString(e);
+            return false;
+        }
+        q.y64 = z;
+        q.y64_stride = count;
+        bool ok = true;
+        for (int part = 0; part < plan.parts && ok; ++part) {
+            DirectParams qp = q;
+            qp.half = p.half - part * plan.ntaps; // partition part covers taps [part * ntaps, ...)
+            qp.peak = part == plan.parts - 1 ? p.peak : nullptr;
+            if (part == 0) ok = fft_launch_one<kFftOutFirst>(plan, qp, part, nch, s, err);
+            else if (part < plan.parts - 1) ok = fft_launch_one<kFftOutAdd>(plan, qp, part, nch, s, err);
+            else ok = fft_launch_one<kFftOutLast>(plan, qp, part, nch, s, err);
+        }
+        e = hipFreeAsync(z, s);
+        if (!ok) return false;
+        if (e != hipSuccess) {
+            err = std::string("partial-sum scratch free: ") + hipGetErrorString(e);
             return false;
         }
     }

@@ -255,7 +255,7 @@ int lcfir_ctx_set_method(lcfir_ctx *ctx, int method) {
         return fail(LCFIR_EINVAL, "unknown method %d", method);
     if (method == LCFIR_METHOD_FFT && !lcfir::fft_supported(ctx->ntaps))
         return fail(LCFIR_EINVAL, "FFT method supports at most %d taps (got %d)",
-                    lcfir::kFftL - lcfir::kFftMinB + 1, ctx->ntaps);
+                    lcfir::kFftMaxTaps, ctx->ntaps);
     ctx->method = method;
     return LCFIR_OK;
 }

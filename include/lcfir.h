@@ -50,7 +50,8 @@ typedef enum lcfir_method {
     LCFIR_METHOD_AUTO = 0,   /* fastest method for the tap count */
     LCFIR_METHOD_DIRECT = 1, /* strict-order f64 FMA chain per output (bit-exact vs the
                                 oracle's ORACLE_FMA restatement) */
-    LCFIR_METHOD_FFT = 2     /* f64 overlap-save FFT convolution */
+    LCFIR_METHOD_FFT = 2     /* f64 overlap-save FFT convolution, any T up to 2^20 taps (longer
+                                than ~10 900 taps: equal partitions summed in f64) */
 } lcfir_method;
 
 /* Progress callback: `count` more samples finished.  Replaces

@@ -304,3 +304,92 @@ def test_fft_channel_beyond_2gib(lc, oracle_mod):
     assert max_ulps(y[0][idx], ref_ld) <= 1
     assert pk[0] == np.abs(y[0]).max()
     assert np.isfinite(y[0]).all()
+
+
+# ---- long filters: the FFT method in partitions (fir_fft.hpp fft_partition_count)
+@pytest.mark.parametrize("ntaps", [10925, 19201, 38401, 100001])
+def test_fft_partitioned_long_filters(lc, oracle_mod, ntaps):
+    """Filters longer than one overlap-save segment favours run as P equal
+    partitions summed in f64 (10 925: 2 partitions just past the cost
+    crossover; 19 201: config 1's kernel; 38 401, 100 001: more partitions).
+    Whole channels through filter_channels_dev and a sub-range through
+    filter_window, against the long-double oracle at every edge sample and
+    random positions; the fused peak against the output."""
+    import synth
+    fs, n, nch = 48000.0, 300_000, 2
+    taps = oracle_mod.design_lowcut(20.0, fs, ntaps)
+    x = synth.file_buffer(nch, n, fs, file=5, bits=24)
+    flt = lc.Filter(taps, method="fft")
+    y, pk = gpu_filter_channels(lc, flt, x)
+    for c in range(nch):
+        idx = _sample_positions(n, ntaps // 2, 2048, 300 + c)
+        ref_ld, _ = oracle_mod.filter_points(x[c], taps, idx, oracle_mod.MODE_LD)
+        assert rms(y[c][idx], ref_ld) <= RMS_TOL
+        assert max_ulps(y[c][idx], ref_ld) <= 1
+        assert pk[c] == np.abs(y[c]).max()
+    # a sub-range from only the input window it needs (a file sharded by sample
+    # range): every partition's shifted reads must stay inside that window
+    half = (ntaps - 1) // 2
+    for start, end in [(12_345, n - 23_456), (half + 7, half + 70_007), (n - 5_000, n)]:
+        yw = gpu_filter_window(lc, flt, x, start, end, max(0, start - half), min(n, end + half))
+        assert np.array_equal(yw, y[:, start:end]), (start, end)
+
+
+def gpu_filter_window(lc, flt, x, start, end, x_lo, x_hi):
+    """Outputs [start, end) of every channel through lcfir_filter_window_dev,
+    given only the samples [x_lo, x_hi) of each channel."""
+    nch, n = x.shape
+    xw = np.ascontiguousarray(x[:, x_lo:x_hi], np.float32)
+    dx = lc.DeviceBuffer.from_array(xw)
+    dy = lc.DeviceBuffer(4 * nch * (end - start))
+    flt.filter_window_dev(dx, x_lo, x_hi, x_hi - x_lo, n, nch, dy, start, end - start, start, end)
+    lc.sync()
+    y = dy.download((nch, end - start))
+    dx.free()
+    dy.free()
+    return y
+
+
+_CHUNK_CHILD = """
+import sys, numpy as np
+sys.path[:0] = [{pkg!r}, {oracle!r}]
+import lcfir, synth
+x = synth.file_buffer(1, {n}, 48000.0, file=6, bits=24)
+taps = np.load({taps!r})
+flt = lcfir.Filter(taps, method="fft")
+dx = lcfir.DeviceBuffer.from_array(x); dy = lcfir.DeviceBuffer(x.nbytes); dpk = lcfir.DeviceBuffer(4)
+lcfir.peak_reset_dev(dpk, 1)
+flt.filter_channels_dev(dx, {n}, 1, {n}, dy, {n}, dpk)
+lcfir.sync()
+np.savez({out!r}, y=dy.download((1, {n})), pk=dpk.download(1))
+"""
+
+
+def test_fft_partitioned_chunk_seams(oracle_mod, tmp_path):
+    """A partitioned filter with launches split into 65 536-output chunks
+    (LCFIR_FFT_CHUNK, read once per process, so in a child process): the f64
+    partial-sum scratch restarts at every seam.  Checked around each seam."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    n, chunk = 400_000, 65_536
+    taps = oracle_mod.design_lowcut(20.0, 48000.0, 19201)
+    np.save(tmp_path / "taps.npy", taps)
+    code = _CHUNK_CHILD.format(pkg=os.path.join(root, "audio-fir-filter_amd"),
+                               oracle=os.path.join(root, "oracle"), n=n,
+                               taps=str(tmp_path / "taps.npy"), out=str(tmp_path / "y.npz"))
+    env = dict(os.environ, LCFIR_FFT_CHUNK=str(chunk))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = np.load(tmp_path / "y.npz")
+    y, pk = d["y"][0], d["pk"][0]
+    import synth
+    x = synth.file_buffer(1, n, 48000.0, file=6, bits=24)[0]
+    seams = np.r_[[s + o for s in range(chunk, n, chunk) for o in range(-3, 3)]]
+    idx = np.unique(np.r_[_sample_positions(n, 9600, 512, 61), seams])
+    ref_ld, _ = oracle_mod.filter_points(x, taps, idx, oracle_mod.MODE_LD)
+    assert rms(y[idx], ref_ld) <= RMS_TOL
+    assert max_ulps(y[idx], ref_ld) <= 1
+    assert pk == np.abs(y).max()
