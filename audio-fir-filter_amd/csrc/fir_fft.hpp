@@ -61,6 +61,27 @@ __device__ unsigned long long g_fft_trace[64][8][24];
     } while (0)
 #endif
 
+// Per-unit timeline for tools/launch_trace.hip (off in the product build):
+// thread 0 of every workgroup records s_memrealtime (100 MHz, chip-wide) at
+// kernel entry (slot 0), at the top of each unit (slots 1..) and at exit.
+#ifdef LCFIR_FFT_UTRACE
+constexpr int kUtraceSlots = 160;
+__device__ unsigned long long g_fft_utrace[1024][kUtraceSlots];
+__device__ unsigned long long g_fft_uclock[1024][2]; // s_memtime (shader clock) at entry, exit
+#define FFT_USTAMP(slot)                                                                    \
+    do {                                                                                    \
+        if (threadIdx.x == 0 && blockIdx.x < 1024) {                                        \
+            g_fft_utrace[blockIdx.x][min((int)(slot), kUtraceSlots - 1)] =                  \
+                __builtin_amdgcn_s_memrealtime();                                           \
+            g_fft_uclock[blockIdx.x][(slot) == 0 ? 0 : 1] = __builtin_amdgcn_s_memtime();   \
+        }                                                                                   \
+    } while (0)
+#else
+#define FFT_USTAMP(slot) \
+    do {                 \
+    } while (0)
+#endif
+
 
 namespace lcfir {
 
@@ -413,12 +434,23 @@ __device__ __forceinline__ void fft_w0_permute_out(double2 (&x0)[8], double2 (&x
     x1[4] = csel(sp, v4, x1[4]);
 }
 
-// Wave max of a running peak, one atomic per wave (channel ch < 0: nothing yet).
-__device__ __forceinline__ void fft_peak_flush(const DirectParams &p, int ch, float pk) {
-    if (!p.peak || ch < 0) return;
+// The fused peak leaves a workgroup as ONE atomic per channel: each wave puts
+// the max of its running per-lane peak into its LDS slot (fft_peak_stage),
+// and after the next workgroup barrier thread 0 folds the 8 slots into one
+// atomicMax (fft_peak_commit).  One atomic per wave -- 2 048 same-address
+// atomics when every workgroup crosses into the next channel in the same
+// round -- stalled that round by ~25 % (tools/launch_trace.hip).
+__device__ __forceinline__ void fft_peak_stage(float *pk_lds, float pk) {
 #pragma unroll
     for (int s = 32; s >= 1; s >>= 1) pk = fmaxf(pk, __shfl_xor(pk, s, 64));
-    if ((threadIdx.x & 63) == 0) atomicMax(p.peak + ch * p.peak_stride, __float_as_uint(pk));
+    if ((threadIdx.x & 63) == 0) pk_lds[threadIdx.x >> 6] = pk;
+}
+// thread 0 only, after a barrier that follows every wave's fft_peak_stage
+__device__ __forceinline__ void fft_peak_commit(const DirectParams &p, int ch, const float *pk_lds) {
+    float pk = pk_lds[0];
+#pragma unroll
+    for (int w = 1; w < kFftNT / 64; ++w) pk = fmaxf(pk, pk_lds[w]);
+    atomicMax(p.peak + ch * p.peak_stride, __float_as_uint(pk));
 }
 
 // Persistent: one workgroup per CU walks the units u = blockIdx.x + i * gridDim.x
@@ -444,6 +476,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
                                                             const uint32_t *__restrict__ task, int B,
                                                             int64_t nseg, int64_t units, double2 c8) {
     extern __shared__ double2 flds[];
+    FFT_USTAMP(0);
     double2 *twl = flds + kFftM; // the kFftTw twiddles, LDS-resident
     for (int i = threadIdx.x; i < kFftTw; i += kFftNT) twl[i] = tw[i];
     float2 v[16]; // samples of the unit about to start
@@ -463,6 +496,8 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     asm volatile("" : "+v"(tk_all));
     float pk_run = 0.0f; // running max |y| of channel pk_ch over this lane's outputs
     int pk_ch = -1;
+    float *pk_lds = reinterpret_cast<float *>(twl + kFftTw); // per-wave peaks (fft_peak_stage)
+    int pk_pending = -1; // channel whose staged per-wave peaks await thread 0's commit
     for (int64_t u = blockIdx.x; u < units; u += gridDim.x) {
     // Laundered thread index: everything derived from it is recomputed per
     // unit instead of being hoisted out of the loop (keeps pressure down).
@@ -476,6 +511,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     const int ch = (int)(u / nseg);
     const int64_t n0 = p.start + (u % nseg) * B;
     FFT_STAMP(0);
+    FFT_USTAMP(1 + (u - blockIdx.x) / gridDim.x);
 
     // ---- stage 1: thread b = j, 16-point DFT over z[512 a + b] -> column c
     {
@@ -493,6 +529,12 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
         for (int c = 0; c < 16; ++c) flds[512 * fft_slot(c) + j] = a[c];
         FFT_STAMP(3);
         __syncthreads();
+        // the previous channel's staged peaks (written before this barrier;
+        // rewritten at the earliest after the next one)
+        if (pk_pending >= 0) {
+            if (threadIdx.x == 0) fft_peak_commit(p, pk_pending, pk_lds);
+            pk_pending = -1;
+        }
         FFT_STAMP(4);
     }
 
@@ -741,19 +783,32 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
             }
         }
     }
-    // fused peak: a running per-lane max, flushed (wave max + one atomic) only
-    // when this workgroup moves to another channel and at the end -- a
-    // per-unit atomic from every wave serialised on the peak slots and cost
-    // ~40 % of the kernel
+    // fused peak: a running per-lane max, staged (fft_peak_stage) only when
+    // this workgroup moves to another channel and at the end -- a per-unit
+    // atomic from every wave serialised on the peak slots and cost ~40 % of
+    // the kernel.  Staging follows this unit's second barrier, so thread 0
+    // has committed the previous staging (after the first) already.
     if (ch != pk_ch) {
-        fft_peak_flush(p, pk_ch, pk_run);
+        if (p.peak && pk_ch >= 0) {
+            fft_peak_stage(pk_lds, pk_run);
+            pk_pending = pk_ch;
+            asm volatile("" : "+v"(pk_pending)); // a VGPR: SGPRs are the scarcer file here
+        }
         pk_run = 0.0f;
         pk_ch = ch;
     }
     pk_run = fmaxf(pk_run, pk);
     FFT_STAMP(14);
     }
-    fft_peak_flush(p, pk_ch, pk_run);
+    FFT_USTAMP(1 + (units - 1 - blockIdx.x) / gridDim.x + 1);
+    if (p.peak && pk_ch >= 0) {
+        __syncthreads();
+        if (pk_pending >= 0 && threadIdx.x == 0) fft_peak_commit(p, pk_pending, pk_lds);
+        __syncthreads();
+        fft_peak_stage(pk_lds, pk_run);
+        __syncthreads();
+        if (threadIdx.x == 0) fft_peak_commit(p, pk_ch, pk_lds);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -892,7 +947,8 @@ inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, hipSt
     return true;
 }
 
-constexpr size_t fft_lds_bytes() { return sizeof(double2) * (size_t)(kFftM + kFftTw); }
+// work array + twiddles + one f32 peak slot per wave
+constexpr size_t fft_lds_bytes() { return sizeof(double2) * (size_t)(kFftM + kFftTw) + 4 * (kFftNT / 64); }
 
 // workgroups per CU the persistent grid assumes (137 KiB of LDS each: one);
 // LCFIR_FFT_BLOCKS_PER_CU overrides for experiments

@@ -14,6 +14,9 @@ normalize decision and rescale (a no-op unless the peak exceeds 1 or
 --normalize).
 
   --config 2  (default) one 10-min file per GPU: weak scaling, no collective
+  --config 3  one 60-s 8-channel 96 kHz float32 file per GPU, 8001 taps (the
+              long-filter stress case; BASELINE.json names no duration, SURVEY.md
+              s8a proposes 60 s)
   --config 4  8 x 60-min files over the ranks (one per GPU at N = 8)
   --config 5  config 4 + --normalize (per-file peaks; --peak-scope global adds
               the RCCL MAX all-reduce of the north-star variant)
@@ -42,7 +45,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", type=int, default=2, choices=[2, 4, 5])
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
     ap.add_argument("--method", default="auto", choices=["auto", "direct", "fft"])
     ap.add_argument("--files", type=int, default=None, help="files in the batch (configs 4/5)")
     ap.add_argument("--seconds", type=float, default=None, help="file length in seconds")
@@ -59,6 +62,9 @@ def parse():
     a = ap.parse_args()
     if a.config == 2:
         a.seconds = 600.0 if a.seconds is None else a.seconds
+    elif a.config == 3:
+        a.seconds = 60.0 if a.seconds is None else a.seconds
+        a.channels, a.fs, a.ntaps, a.bits = 8, 96000.0, 8001, 0
     else:
         a.files = 8 if a.files is None else a.files
         a.seconds = 3600.0 if a.seconds is None else a.seconds
@@ -184,7 +190,8 @@ def main():
 
     nch, fs = args.channels, args.fs
     n = int(round(args.seconds * fs))
-    nfiles = world if args.config == 2 else args.files
+    per_gpu = args.config in (2, 3)  # one file per rank (weak scaling)
+    nfiles = world if per_gpu else args.files
     taps = design_taps(args.ntaps, fs)
     half = (args.ntaps - 1) // 2
     bits = args.bits or None
@@ -198,7 +205,7 @@ def main():
     cache = {}
 
     def file_samples(f):
-        key = f if args.config == 2 else f % 2
+        key = f if per_gpu else f % 2
         if key not in cache:
             cache[key] = synth.file_buffer(nch, n, fs, file=key, bits=bits)
         return cache[key]
@@ -265,6 +272,7 @@ def main():
         fp64_tflops = f64_flops / kern_s / 1e12 if f64_flops else None
         valu_frac = valu_insts * VALU_NS_PER_INST * 1e-9 / (simds * kern_s) if valu_insts else None
         wl = {2: "config2: 10 min stereo 48 kHz int24 file per GPU",
+              3: f"config3: {args.seconds:g} s 8-channel 96 kHz float32 file per GPU",
               4: f"config4: {nfiles} x {args.seconds / 60:g} min stereo 48 kHz int24 files",
               5: f"config5: {nfiles} x {args.seconds / 60:g} min stereo 48 kHz int24 files, "
                  f"--normalize"}
@@ -277,10 +285,11 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak" if args.config == 2 else "strong",
+            "scaling": "weak" if per_gpu else "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (SURVEY.md s8d int24 generator), resident in HBM",
+            "data": f"synthetic (SURVEY.md s8d {'int%d' % bits if bits else 'float32'} generator), "
+                    f"resident in HBM",
             "config": {
                 "workload": wl[args.config] + f", {args.ntaps}-tap low-cut",
                 "files": nfiles, "channels": nch, "samples_per_channel": n,
