@@ -95,6 +95,11 @@ class Backend:
         """rescale by 1/peak iff peak > 1 or force; slot None = max over all slots."""
         raise NotImplementedError
 
+    def normalize_clear(self, yw, nch, count, peaks, slot: Optional[int], force: bool, clear):
+        """normalize, then zero the (separate) peak vector `clear`."""
+        self.normalize(yw, nch, count, peaks, slot, force)
+        self.zero_peaks(clear)
+
     def new_peaks(self, nfiles: int):
         raise NotImplementedError
 
@@ -124,13 +129,20 @@ class BatchRunner:
         if self.exchange and allreduce_max is None:
             raise ValueError("this plan needs a MAX all-reduce of the peak vector")
         self.allreduce_max = allreduce_max
-        self.peaks = backend.new_peaks(len(self.nframes))
+        # two peak vectors, alternating by step: a step's last normalize
+        # launch also zeroes the other one for the next step, so no separate
+        # reset launch sits in the step
+        self._peak_bufs = [backend.new_peaks(len(self.nframes)) for _ in range(2)]
+        self._cur = 0
+        self.peaks = self._peak_bufs[0]  # the most recent step's per-file peaks
         self.inputs = []
         self.outputs = []
 
     def prepare(self, get_window: Callable):
         """get_window(file, x_lo, x_hi) -> [nch][x_hi - x_lo] float32 samples."""
         self.inputs, self.outputs = [], []
+        for pk in self._peak_bufs:
+            self.b.zero_peaks(pk)
         for sh in self.shards:
             n = self.nframes[sh.file]
             lo, hi = window(sh, n, self.half)
@@ -138,15 +150,25 @@ class BatchRunner:
             self.outputs.append(self.b.alloc_out(self.nch, sh.end - sh.start))
 
     def step(self):
-        self.b.zero_peaks(self.peaks)
+        peaks = self._peak_bufs[self._cur]      # zero (prepare, or the previous step)
+        nxt = self._peak_bufs[1 - self._cur]
         for sh, (xw, lo, hi), yw in zip(self.shards, self.inputs, self.outputs):
             self.b.filter(xw, lo, hi, self.nframes[sh.file], self.nch, yw, sh.start, sh.end,
-                          self.peaks, sh.file)
+                          peaks, sh.file)
         if self.exchange:
-            self.allreduce_max(self.peaks)
-        for sh, yw in zip(self.shards, self.outputs):
+            self.allreduce_max(peaks)
+        last = len(self.shards) - 1
+        for i, (sh, yw) in enumerate(zip(self.shards, self.outputs)):
             slot = None if self.scope == "global" else sh.file
-            self.b.normalize(yw, self.nch, sh.end - sh.start, self.peaks, slot, self.normalize)
+            if i == last:
+                self.b.normalize_clear(yw, self.nch, sh.end - sh.start, peaks, slot, self.normalize,
+                                       nxt)
+            else:
+                self.b.normalize(yw, self.nch, sh.end - sh.start, peaks, slot, self.normalize)
+        if not self.shards:
+            self.b.zero_peaks(nxt)
+        self.peaks = peaks
+        self._cur = 1 - self._cur
 
     def results(self):
         """[(shard, output handle)] for this rank."""
@@ -184,6 +206,11 @@ class DeviceBackend(Backend):
     def normalize(self, yw, nch, count, peaks, slot, force):
         p = peaks if slot is None else peaks[slot:slot + 1]
         self.lc.normalize_dev(yw, yw.shape[1], nch, count, p, p.numel(), force, self.sp)
+
+    def normalize_clear(self, yw, nch, count, peaks, slot, force, clear):
+        p = peaks if slot is None else peaks[slot:slot + 1]
+        self.lc.normalize_clear_dev(yw, yw.shape[1], nch, count, p, p.numel(), force, clear,
+                                    clear.numel(), self.sp)
 
 
 def torch_allreduce_max(group=None):

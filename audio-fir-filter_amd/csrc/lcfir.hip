@@ -438,20 +438,28 @@ int lcfir_peak_dev(const float *d_y, int64_t stride, int32_t nch, int64_t n, flo
     return LCFIR_OK;
 }
 
-int lcfir_normalize_dev(float *d_y, int64_t stride, int32_t nch, int64_t n, const float *d_peak,
-                        int32_t npeak, int force, void *stream) {
-    if (!d_y || !d_peak || nch < 0 || n < 0 || npeak < 1)
+int lcfir_normalize_clear_dev(float *d_y, int64_t stride, int32_t nch, int64_t n, const float *d_peak,
+                              int32_t npeak, int force, float *d_clear, int32_t nclear, void *stream) {
+    if (!d_y || !d_peak || nch < 0 || n < 0 || npeak < 1 || nclear < 0 || (nclear > 0 && !d_clear))
         return fail(LCFIR_EINVAL, "bad argument");
-    if (nch == 0 || n == 0) return LCFIR_OK;
     if (nch > 65535) return fail(LCFIR_EINVAL, "too many channels");
+    if (nclear > 0 && d_clear < d_peak + npeak && d_peak < d_clear + nclear)
+        return fail(LCFIR_EINVAL, "the slots to clear overlap the peak slots read");
+    if (nch == 0 || n == 0) return nclear > 0 ? lcfir_peak_reset_dev(d_clear, nclear, stream) : LCFIR_OK;
     // grid-stride: 256 blocks per channel already saturate HBM when the pass
     // rescales, and keep the (common) no-op launch short
     const int blocks = std::min(stream_blocks(n, 256 * 16), 256);
     hipLaunchKernelGGL(lcfir::normalize_kernel, dim3(blocks, nch), dim3(256), 0,
                        reinterpret_cast<hipStream_t>(stream), d_y, stride, n,
-                       reinterpret_cast<const unsigned *>(d_peak), npeak, force);
+                       reinterpret_cast<const unsigned *>(d_peak), npeak, force,
+                       nclear > 0 ? peak_bits(d_clear) : nullptr, nclear);
     LCFIR_HIP(hipGetLastError());
     return LCFIR_OK;
+}
+
+int lcfir_normalize_dev(float *d_y, int64_t stride, int32_t nch, int64_t n, const float *d_peak,
+                        int32_t npeak, int force, void *stream) {
+    return lcfir_normalize_clear_dev(d_y, stride, nch, n, d_peak, npeak, force, nullptr, 0, stream);
 }
 
 int lcfir_channel_peak(int device, const float *y, int64_t n, float *peak) {

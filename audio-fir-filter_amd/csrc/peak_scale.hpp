@@ -50,10 +50,15 @@ __device__ __forceinline__ float scale_one(float v, double gain) {
 }
 
 // Normalize: the decision is taken on the device from d_peak, so no host
-// round trip sits between the filter and the rescale.
+// round trip sits between the filter and the rescale.  Block (0, 0) also
+// zeroes clear[0, nclear) -- the next step's peak slots (a separate buffer),
+// which saves the batch driver one launch per step.
 __global__ __launch_bounds__(256) void normalize_kernel(float *__restrict__ y, int64_t stride,
                                                         int64_t n, const unsigned *__restrict__ peak,
-                                                        int npeak, int force) {
+                                                        int npeak, int force, unsigned *__restrict__ clear,
+                                                        int nclear) {
+    if (blockIdx.x == 0 && blockIdx.y == 0)
+        for (int i = threadIdx.x; i < nclear; i += blockDim.x) clear[i] = 0u;
     float pk = 0.0f;
     for (int i = 0; i < npeak; ++i) pk = fmaxf(pk, __uint_as_float(peak[i]));
     if (!(pk > 1.0f || force) || !(pk > 0.0f)) return;

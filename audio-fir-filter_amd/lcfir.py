@@ -64,6 +64,8 @@ _SIGNATURES = {
     "lcfir_peak_reset_dev": ([_vp, _c_i32, _vp], _c_int),
     "lcfir_peak_dev": ([_vp, _c_i64, _c_i32, _c_i64, _vp, _vp], _c_int),
     "lcfir_normalize_dev": ([_vp, _c_i64, _c_i32, _c_i64, _vp, _c_i32, _c_int, _vp], _c_int),
+    "lcfir_normalize_clear_dev": (
+        [_vp, _c_i64, _c_i32, _c_i64, _vp, _c_i32, _c_int, _vp, _c_i32, _vp], _c_int),
     "lcfir_channel_peak": ([_c_int, _vp, _c_i64, ctypes.POINTER(ctypes.c_float)], _c_int),
     "lcfir_design_lowcut": ([ctypes.c_double, ctypes.c_double, ctypes.c_double, _vp, _c_i32,
                              ctypes.POINTER(_c_i32)], _c_int),
@@ -308,6 +310,14 @@ def peak_dev(d_y, stride: int, nch: int, n: int, d_peak, stream=0):
 def normalize_dev(d_y, stride: int, nch: int, n: int, d_peak, npeak: int, force: bool, stream=0):
     _check(load().lcfir_normalize_dev(_ptr(d_y), stride, nch, n, _ptr(d_peak), npeak,
                                       1 if force else 0, stream or None))
+
+
+def normalize_clear_dev(d_y, stride: int, nch: int, n: int, d_peak, npeak: int, force: bool,
+                        d_clear, nclear: int, stream=0):
+    """normalize_dev that also zeroes d_clear[0:nclear] in the same launch."""
+    _check(load().lcfir_normalize_clear_dev(_ptr(d_y), stride, nch, n, _ptr(d_peak), npeak,
+                                            1 if force else 0, _ptr(d_clear) if nclear else None,
+                                            nclear, stream or None))
 
 
 def channel_peak(y: np.ndarray, device: int = 0) -> float:

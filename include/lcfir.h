@@ -125,6 +125,13 @@ int lcfir_peak_dev(const float *d_y, int64_t stride, int32_t nch, int64_t n, flo
  * c_lib's AudioSamples::normalize is unpinned. */
 int lcfir_normalize_dev(float *d_y, int64_t stride, int32_t nch, int64_t n,
                         const float *d_peak, int32_t npeak, int force, void *stream);
+/* lcfir_normalize_dev that also zeroes d_clear[0..nclear) in the same launch
+ * (a batch driver's next-step peak slots: one launch per step fewer than a
+ * separate lcfir_peak_reset_dev).  d_clear must not overlap d_peak[0..npeak)
+ * (LCFIR_EINVAL).  nclear 0 = lcfir_normalize_dev. */
+int lcfir_normalize_clear_dev(float *d_y, int64_t stride, int32_t nch, int64_t n,
+                              const float *d_peak, int32_t npeak, int force, float *d_clear,
+                              int32_t nclear, void *stream);
 /* Host-pointer convenience: max|y| of one channel (VectorMath::max_mag). */
 int lcfir_channel_peak(int device, const float *y, int64_t n, float *peak);
 

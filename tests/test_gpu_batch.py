@@ -86,3 +86,35 @@ def test_device_batch_runner(tt, oracle_mod, normalize, loud):
         oracle_mod.process_buffer(ref, taps, nthreads=1, normalize=normalize,
                                   mode=oracle_mod.MODE_FMA)
         assert np.array_equal(y.cpu().numpy(), ref[:, sh.start:sh.end])
+
+
+def test_normalize_clear_dev(tt):
+    """lcfir_normalize_clear_dev = lcfir_normalize_dev + zeroing a separate
+    peak vector in the same launch (the batch driver's next-step slots)."""
+    torch, lc = tt
+    rng = np.random.default_rng(3)
+    y0 = (rng.standard_normal((2, 5003)) * 1.5).astype(np.float32)
+    pk = float(np.abs(y0).max())
+    dev = torch.device("cuda", 0)
+    peaks = torch.tensor([0.25, pk, 0.5], dtype=torch.float32, device=dev)
+    for force in (False, True):
+        ya = torch.from_numpy(y0).to(dev)
+        yb = ya.clone()
+        clear = torch.full((5,), 7.0, dtype=torch.float32, device=dev)
+        lc.normalize_dev(ya, 5003, 2, 5003, peaks, 3, force)
+        lc.normalize_clear_dev(yb, 5003, 2, 5003, peaks, 3, force, clear, 4)
+        torch.cuda.synchronize()
+        assert torch.equal(ya, yb)
+        assert clear.cpu().tolist() == [0.0, 0.0, 0.0, 0.0, 7.0]
+        assert peaks.cpu().tolist()[1] == pk  # the slots read are left alone
+    ref = (y0.astype(np.float64) * (1.0 / pk)).astype(np.float32)
+    assert np.array_equal(yb.cpu().numpy(), ref)
+    # nothing to rescale (nch = 0): the slots are still cleared
+    clear = torch.full((3,), 7.0, dtype=torch.float32, device=dev)
+    lc.normalize_clear_dev(yb, 5003, 0, 5003, peaks, 3, False, clear, 3)
+    torch.cuda.synchronize()
+    assert clear.cpu().tolist() == [0.0, 0.0, 0.0]
+    # the slots to clear must not overlap the slots read
+    with pytest.raises(lc.LcfirError) as e:
+        lc.normalize_clear_dev(yb, 5003, 2, 5003, peaks, 3, False, peaks[2:], 1)
+    assert "overlap" in str(e.value)
