@@ -30,7 +30,7 @@ int main(int argc, char **argv) {
     const int64_t n = argc > 1 ? std::atoll(argv[1]) : 28800000;
     const int reps = argc > 2 ? std::atoi(argv[2]) : 10;
     const int sets = argc > 3 ? std::max(1, std::atoi(argv[3])) : 1; // buffer sets rotated over launches
-    const int nch = 2, T = 4001;
+    const int nch = argc > 5 ? std::atoi(argv[5]) : 2, T = 4001;
     std::vector<float> hx((size_t)n * nch);
     uint64_t s = 12345;
     for (auto &v : hx) {
