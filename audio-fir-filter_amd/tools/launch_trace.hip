@@ -26,6 +26,12 @@
         }                                                                       \
     } while (0)
 
+// one wave busy-waiting `ticks` of the 100 MHz clock: an almost idle GPU between launches
+__global__ void spin_kernel(long long ticks) {
+    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+    while ((long long)__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
+}
+
 int main(int argc, char **argv) {
     const int64_t n = argc > 1 ? std::atoll(argv[1]) : 28800000;
     const int reps = argc > 2 ? std::atoi(argv[2]) : 10;
@@ -85,7 +91,11 @@ int main(int argc, char **argv) {
     CK(hipEventCreate(&e1));
     for (int it = 0; it < 3; ++it) launch();
     CK(hipEventRecord(e0));
-    for (int it = 0; it < reps; ++it) launch();
+    const int gap_us = argc > 6 ? std::atoi(argv[6]) : 0; // > 0: a spin kernel of ~gap_us between launches
+    for (int it = 0; it < reps; ++it) {
+        launch();
+        if (gap_us > 0) hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, nullptr, (long long)gap_us * 100);
+    }
     CK(hipEventRecord(e1));
     CK(hipEventSynchronize(e1));
     float ms = 0;
