@@ -100,7 +100,10 @@ constexpr int kVmcnt0 = 0x0F70;     // s_waitcnt vmcnt(0) (expcnt, lgkmcnt left 
 // sample loads measured 0 to -5 %, so those stay cached)
 constexpr int kNtStore = 2;
 // output modes of fir_fft_f64_kernel (see there)
-constexpr int kFftOutF32 = 0, kFftOutFirst = 1, kFftOutAdd = 2, kFftOutLast = 3;
+constexpr int kFftOutF32 = 0, kFftOutFirst = 1, kFftOutAdd = 2, kFftOutLast = 3, kFftOutSym = 4;
+// kFftOutSym = kFftOutF32 for a linear-phase filter in zero-phase form: real
+// pair table (fft_plan_build's symmetric layout), outputs c in [half, L - half)
+constexpr int kFftSymS2 = 0, kFftSymD2 = 8 * kFftNT, kFftSymW = 8 * kFftNT; // doubles, doubles, double2
 
 // Wave 0, lanes 32..63: the column-0 task pairs (d1A | e1A << 3 | d1B << 6 |
 // e1B << 9), ordered so the exchange-2 reads and exchange-3 writes stay
@@ -127,7 +130,29 @@ struct FftPlan {
     double2 *d_tw = nullptr;   // kFftTw twiddles
     uint32_t *d_task = nullptr; // [512] task words (cA, d1A, e1A, cB, d1B, e1B)
     int cus = 256;             // compute units of the plan's device (persistent grid)
+    bool sym = false;          // linear-phase filter run in zero-phase form (kFftOutSym)
 };
+
+// A filter runs in zero-phase form (kFftOutSym: real pair table, a cheaper
+// pair step) when it is one partition, half = (T-1)/2 is even (the output
+// pairs stay 8-byte aligned) and it is symmetric, h[k] = h[T-1-k], up to an
+// antisymmetric part of at most 2^-50 of its l1 norm.  Dropping that part
+// changes any output by at most 2^-50 |h|_1 max|x| -- the size of the f64
+// FFT's own rounding error.  LCFIR_FFT_SYM=0 turns the form off.
+inline bool fft_sym_eligible(const std::vector<double> &h, int parts) {
+    static const bool on = [] {
+        const char *e = std::getenv("LCFIR_FFT_SYM");
+        return !(e && e[0] == '0');
+    }();
+    const int T = (int)h.size();
+    if (!on || parts != 1 || T < 3 || ((T - 1) / 2) % 2 != 0) return false;
+    long double anti = 0.0L, norm = 0.0L;
+    for (int k = 0; k < T; ++k) {
+        anti += fabsl(((long double)h[(size_t)k] - (long double)h[(size_t)(T - 1 - k)]) * 0.5L);
+        norm += fabsl((long double)h[(size_t)k]);
+    }
+    return norm > 0.0L && anti <= norm * 0x1p-50L;
+}
 
 inline bool fft_supported(int ntaps) { return ntaps >= 1 && ntaps <= kFftMaxTaps; }
 inline bool fft_preferred(int ntaps) { return ntaps >= 96 && fft_supported(ntaps); }
@@ -399,6 +424,17 @@ __device__ __forceinline__ void fft_pair(double2 P, double2 Q, double2 W, double
     oQ = csub(cmul(Zm, Q2), cmul(P, P2));
 }
 
+// The same pair for a linear-phase (symmetric) filter in zero-phase form
+// (kFftOutSym): G is real, so 2S = s2 and 2D = d2 are real, P1 and Q2 real and
+// P2 = i p2 imaginary -- 11 f64 operations instead of ~26.
+__device__ __forceinline__ void fft_pair_sym(double2 P, double2 Q, double2 W, double s2, double d2,
+                                             double2 &oP, double2 &oQ) {
+    const double p1 = __builtin_fma(d2, W.y, s2), q2 = __builtin_fma(-d2, W.y, s2), p2 = d2 * W.x;
+    // oP = conj(P p1 + conj(Q) i p2),  oQ = conj(Q) q2 - P i p2
+    oP = make_double2(__builtin_fma(p1, P.x, p2 * Q.y), -__builtin_fma(p1, P.y, p2 * Q.x));
+    oQ = make_double2(__builtin_fma(q2, Q.x, p2 * P.y), -__builtin_fma(q2, Q.y, p2 * P.x));
+}
+
 // Wave 0's special lane (kFftSpecialLane) holds the self-paired tasks: A =
 // column-0 task (d1, e1) = (0, 4), bins 512 + 1024 e2, pairs (A_i, A_7-i); B =
 // task (0, 0), bins 1024 e2, pairs (B_i, B_8-i) with B_0 and B_4 self-paired.
@@ -586,10 +622,21 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     wave_lds_sync();
     FFT_STAMP(6);
     // ---- pair-table loads, issued ahead of stage C (L2 latency off the path)
-    double2 qs[8], qd[8]; // 2 S and 2 D of the pair in slot i
-    const double2 wbase = pair[2 * kFftPairSlots * 512 + j]; // W_L^k of slot 0
-    {
+    constexpr bool kSym = kOut == kFftOutSym;
+    double2 qs[kSym ? 1 : 8], qd[kSym ? 1 : 8]; // 2 S and 2 D of the pair in slot i
+    double qsr[8], qdr[8];                       // kSym: the real 2 S and 2 D
+    double2 wbase;                               // W_L^k of slot 0
+    if constexpr (kSym) {
+        const double *t = reinterpret_cast<const double *>(pair) + j;
+        wbase = pair[kFftSymW + j];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            qsr[i] = t[kFftSymS2 + 512 * i];
+            qdr[i] = t[kFftSymD2 + 512 * i];
+        }
+    } else {
         const double2 *t = pair + j;
+        wbase = pair[2 * kFftPairSlots * 512 + j];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             qs[i] = t[512 * i];
@@ -632,7 +679,12 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
         }
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            fft_pair(x0[i], x1[7 - i], fft_pair_w(i < 4 ? wbase : wb_hi, i), qs[i], qd[i], x0[i], x1[7 - i]);
+            if constexpr (kSym)
+                fft_pair_sym(x0[i], x1[7 - i], fft_pair_w(i < 4 ? wbase : wb_hi, i), qsr[i], qdr[i], x0[i],
+                             x1[7 - i]);
+            else
+                fft_pair(x0[i], x1[7 - i], fft_pair_w(i < 4 ? wbase : wb_hi, i), qs[i], qd[i], x0[i],
+                         x1[7 - i]);
             __builtin_amdgcn_sched_barrier(0);
         }
         if (w0) fft_w0_permute_out(x0, x1, sp, v4);
@@ -720,20 +772,23 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     float *yb = p.y + (int64_t)ch * p.y_stride + (p.start - p.y_lo);
     const __amdgpu_buffer_rsrc_t ys = __builtin_amdgcn_make_buffer_rsrc(
         yb, (short)0, (int)((p.end - p.start) * 4), 0x00020000);
-    const int cmin = p.ntaps - 1;
+    // valid outputs c in [cmin, cmax): [T-1, L) for the causal table, [half,
+    // L - half) for the zero-phase one (kSym: half even, fft_plan_build)
+    const int cmin = kSym ? p.half : p.ntaps - 1;
+    const int cmax = kSym ? kFftL - p.half : kFftL;
     const int64_t off = n0 - cmin - p.start; // offset (samples) of c[0] from start
     const int64_t oend = p.end - p.start;
     float pk = 0.0f;
-    if constexpr (kOut == kFftOutF32) {
-    if (n0 - cmin + kFftL <= p.end) {
+    if constexpr (kOut == kFftOutF32 || kSym) {
+    if (n0 + B <= p.end) {
         // every output of this unit is before `end`: the pair (c, c+1) is
-        // valid iff c >= cmin (cmin and o are even), so both stores share one
-        // offset and may merge into a dwordx2
+        // valid iff cmin <= c < cmax (cmin, cmax and o are even), so both
+        // stores share one offset and may merge into a dwordx2
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int c = 2 * (j + 512 * r);
             const float f0 = (float)a[r].x, f1 = (float)(-a[r].y);
-            const bool ok = c >= cmin;
+            const bool ok = c >= cmin && (!kSym || c < cmax);
             const int ob = ok ? (int)((off + c) * 4) : (int)0x80000000;
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(f0), ys, ob, 0, kNtStore);
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(f1), ys, ob + 4, 0, kNtStore);
@@ -745,7 +800,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
             const int c = 2 * (j + 512 * r);
             const float f0 = (float)a[r].x, f1 = (float)(-a[r].y);
             const int64_t o = off + c;
-            const bool ok0 = c >= cmin && o < oend, ok1 = c + 1 >= cmin && o + 1 < oend;
+            const bool ok0 = c >= cmin && c < cmax && o < oend, ok1 = c + 1 >= cmin && c + 1 < cmax && o + 1 < oend;
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(f0), ys,
                                                   ok0 ? (int)(o * 4) : (int)0x80000000, 0, kNtStore);
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(f1), ys,
@@ -867,6 +922,7 @@ inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, hipSt
     }
     const int parts = fft_partition_count(ntaps);
     const int tp = parts == 1 ? ntaps : fft_partition_taps(ntaps, parts);
+    const bool sym = fft_sym_eligible(taps, parts);
     const long double scale = 1.0L / (4.0L * (long double)kFftM);
     const long double two_pi = 6.283185307179586476925286766559L;
     // pair tables in consumption order: slot i of thread t holds bin k_i of
@@ -883,9 +939,18 @@ inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, hipSt
         // the filter's end), zero padded; scaled by 1/(4M)
         std::fill(re.begin(), re.end(), 0.0L);
         std::fill(im.begin(), im.end(), 0.0L);
-        for (int i = 0; i < tp; ++i) {
-            const int64_t k = (int64_t)part * tp + (tp - 1 - i);
-            re[(size_t)i] = k < ntaps ? (long double)taps[(size_t)k] : 0.0L;
+        if (!sym) {
+            for (int i = 0; i < tp; ++i) {
+                const int64_t k = (int64_t)part * tp + (tp - 1 - i);
+                re[(size_t)i] = k < ntaps ? (long double)taps[(size_t)k] : 0.0L;
+            }
+        } else {
+            // zero-phase form: g[j mod L] = h_sym[half + j], j in [-half, half],
+            // h_sym = (h + reversed h) / 2 -- real and even, so G is real
+            const int half = (ntaps - 1) / 2;
+            for (int j = -half; j <= half; ++j)
+                re[(size_t)((j + kFftL) % kFftL)] =
+                    ((long double)taps[(size_t)(half + j)] + (long double)taps[(size_t)(half - j)]) * 0.5L;
         }
         detail::fft_ld(re, im);
         double2 *pt = pair.data() + (size_t)part * kFftPairTable;
@@ -906,14 +971,20 @@ inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, hipSt
                 const long double a = -two_pi * (long double)k / (long double)kFftL;
                 const long double c = cosl(a), sn = sinl(a); // W = c + i sn
                 const size_t o = (size_t)i * kFftNT + (size_t)t;
-                pt[o] = cplx(2 * sr, 2 * si);
-                pt[(size_t)kFftPairSlots * kFftNT + o] = cplx(2 * dr, 2 * di);
-                pt[(size_t)2 * kFftPairSlots * kFftNT + o] = cplx(c, sn);
+                if (!sym) {
+                    pt[o] = cplx(2 * sr, 2 * si);
+                    pt[(size_t)kFftPairSlots * kFftNT + o] = cplx(2 * dr, 2 * di);
+                    pt[(size_t)2 * kFftPairSlots * kFftNT + o] = cplx(c, sn);
+                } else if (i < 8) {
+                    // symmetric layout: real 2S, 2D per (slot, thread), W of slot 0
+                    double *pd = reinterpret_cast<double *>(pt);
+                    pd[(size_t)kFftSymS2 + o] = (double)(2 * sr);
+                    pd[(size_t)kFftSymD2 + o] = (double)(2 * dr);
+                    if (i == 0) pt[(size_t)kFftSymW + (size_t)t] = cplx(c, sn);
+                }
+                if (i == 8 && sp) c8[(size_t)part] = cplx(2 * sr - 2 * dr, sym ? 0.0L : 2 * si - 2 * di);
             }
         }
-        const size_t o = (size_t)8 * kFftNT + kFftSpecialLane; // slot 8 of the special lane
-        const double2 s2 = pt[o], d2 = pt[(size_t)kFftPairSlots * kFftNT + o];
-        c8[(size_t)part] = make_double2(s2.x - d2.x, s2.y - d2.y);
     }
     std::vector<double2> tw((size_t)kFftTw);
     for (int i = 0; i < 512; ++i) {
@@ -946,6 +1017,7 @@ inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, hipSt
         plan.cus = cus;
     plan.ntaps = tp;
     plan.parts = parts;
+    plan.sym = sym;
     plan.B = kFftL - tp + 1;
     plan.c8 = std::move(c8);
     plan.ready = true;
@@ -1029,7 +1101,9 @@ inline bool fft_launch(const FftPlan &plan, const DirectParams &p, int nch, hipS
         q.x_hi = hi;
         q.ntaps = plan.ntaps;
         if (plan.parts == 1) {
-            if (!fft_launch_one<kFftOutF32>(plan, q, 0, nch, s, err)) return false;
+            if (plan.sym ? !fft_launch_one<kFftOutSym>(plan, q, 0, nch, s, err)
+                         : !fft_launch_one<kFftOutF32>(plan, q, 0, nch, s, err))
+                return false;
             continue;
         }
         const int64_t count = q.end - q.start;
