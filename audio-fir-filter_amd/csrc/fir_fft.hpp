@@ -46,13 +46,12 @@
 
 // Phase timestamps for tools/fft_trace.hip (off in the product build): lane 0
 // of every wave of workgroups < 64 records s_memtime at each phase boundary of
-// its 5th unit.
+// its 5th unit (round 4).
 #ifdef LCFIR_FFT_TRACE
 __device__ unsigned long long g_fft_trace[64][8][24];
 #define FFT_STAMP(i)                                                                     \
     do {                                                                                 \
-        if (blockIdx.x < 64 && u == (int64_t)blockIdx.x + 4 * (int64_t)gridDim.x &&      \
-            (threadIdx.x & 63) == 0)                                                     \
+        if (blockIdx.x < 64 && rnd == 4 && (threadIdx.x & 63) == 0)                      \
             g_fft_trace[blockIdx.x][threadIdx.x >> 6][i] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 #else
@@ -187,6 +186,17 @@ __host__ __device__ constexpr int fft_slot(int c) {
     return c == 0 ? 0 : c == 8 ? 1 : c < 8 ? 2 * c : 33 - 2 * c;
 }
 constexpr int fft_slot_column(int s) { return s == 0 ? 0 : s == 1 ? 8 : s % 2 == 0 ? s / 2 : (33 - s) / 2; }
+
+// Unit processed by workgroup b in round i of a persistent grid of g
+// workgroups.  Workgroups are dealt to the 8 XCDs round-robin (b mod 8), so
+// XCD x gets the g/8 consecutive units i g + x g/8 + (b div 8): a segment and
+// its neighbour share the T-1 halo samples, and on one XCD the second read of
+// the halo hits that XCD's L2 instead of HBM.  A bijection on every round, so
+// the last, partial round still covers [i g, units) exactly.
+__host__ __device__ inline int64_t fft_unit(int64_t i, int b, int g) {
+    if (g % 8 != 0) return i * g + b;
+    return i * g + (int64_t)(b % 8) * (g / 8) + b / 8;
+}
 
 // Task word of thread t = 64 w + lane after exchange 2: task A = (cA, d1A, e1A),
 // task B = (cB, d1B, e1B); bins k = c + 16 (d1 + 8 e1 + 64 e2), e2 = register.
@@ -522,7 +532,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     for (int i = threadIdx.x; i < kFftTw; i += kFftNT) twl[i] = tw[i];
     float2 v[16]; // samples of the unit about to start
     {
-        const int64_t u = blockIdx.x;
+        const int64_t u = fft_unit(0, blockIdx.x, gridDim.x); // < units: the grid is <= units
         fft_load_unit(p, (int)(u / nseg), p.start + (u % nseg) * B, threadIdx.x, v);
     }
     // vmcnt counts loads and stores together, in issue order, and the wait
@@ -539,7 +549,8 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     int pk_ch = -1;
     float *pk_lds = reinterpret_cast<float *>(twl + kFftTw); // per-wave peaks (fft_peak_stage)
     int pk_pending = -1; // channel whose staged per-wave peaks await thread 0's commit
-    for (int64_t u = blockIdx.x; u < units; u += gridDim.x) {
+    int64_t rnd = 0; // round: this workgroup's unit ordinal
+    for (int64_t u = fft_unit(0, blockIdx.x, gridDim.x); u < units; u = fft_unit(++rnd, blockIdx.x, gridDim.x)) {
     // Laundered thread index: everything derived from it is recomputed per
     // unit instead of being hoisted out of the loop (keeps pressure down).
     int j = threadIdx.x;
@@ -552,7 +563,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     const int ch = (int)(u / nseg);
     const int64_t n0 = p.start + (u % nseg) * B;
     FFT_STAMP(0);
-    FFT_USTAMP(1 + (u - blockIdx.x) / gridDim.x);
+    FFT_USTAMP(1 + rnd);
 
     // ---- stage 1: thread b = j, 16-point DFT over z[512 a + b] -> column c
     {
@@ -695,7 +706,8 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     // Unconditional (the last unit reloads itself): a conditional load would
     // keep the old v live across the whole loop body.
     {
-        const int64_t un = u + gridDim.x < units ? u + gridDim.x : u;
+        const int64_t un1 = fft_unit(rnd + 1, blockIdx.x, gridDim.x);
+        const int64_t un = un1 < units ? un1 : u;
         fft_load_unit(p, (int)(un / nseg), p.start + (un % nseg) * B, j, v);
     }
 
@@ -860,7 +872,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     pk_run = fmaxf(pk_run, pk);
     FFT_STAMP(14);
     }
-    FFT_USTAMP(1 + (units - 1 - blockIdx.x) / gridDim.x + 1);
+    FFT_USTAMP(1 + rnd);
     if (p.peak && pk_ch >= 0) {
         __syncthreads();
         if (pk_pending >= 0 && threadIdx.x == 0) fft_peak_commit(p, pk_pending, pk_lds);

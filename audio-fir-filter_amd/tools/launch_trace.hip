@@ -116,7 +116,8 @@ int main(int argc, char **argv) {
     std::vector<double> startd;
     for (int b = 0; b < grid; ++b) t0 = std::min(t0, tr[b][0]);
     for (int b = 0; b < grid; ++b) {
-        const int nu = (int)((units - 1 - b) / grid + 1);
+        int nu = 0;
+        while (lcfir::fft_unit(nu, b, grid) < units) ++nu;
         if (nu + 1 >= kUtraceSlots) {
             std::fprintf(stderr, "too many units per workgroup for the trace\n");
             return 1;
@@ -148,7 +149,8 @@ int main(int argc, char **argv) {
     CK(hipMemcpyFromSymbol(ck, HIP_SYMBOL(g_fft_uclock), sizeof(ck)));
     double ghz = 0;
     for (int b = 0; b < grid; ++b) {
-        const int nu = (int)((units - 1 - b) / grid + 1);
+        int nu = 0;
+        while (lcfir::fft_unit(nu, b, grid) < units) ++nu;
         ghz += (double)(ck[b][1] - ck[b][0]) / (double)(tr[b][nu + 1] - tr[b][0]) * 0.1;
     }
     std::printf("shader clock (s_memtime / s_memrealtime): %.3f GHz\n", ghz / grid);
