@@ -340,6 +340,24 @@ __device__ __forceinline__ void twiddle16(double2 (&a)[16], double2 w1) {
     a[15] = cmul(a[15], cmul(wo, w2));
 }
 
+// w[r] = w1^r, r = 1..15, by twiddle16's chain (the same values, bit for bit)
+__device__ __forceinline__ void powers16(double2 w1, double2 (&w)[16]) {
+    const double2 w2 = cmul(w1, w1);
+    w[1] = w1;
+    w[2] = w2;
+#pragma unroll
+    for (int r = 3; r < 15; r += 2) {
+        w[r] = cmul(w[r - 2], w2);
+        w[r + 1] = cmul(w[r - 1], w2);
+    }
+    w[15] = cmul(w[13], w2);
+}
+
+__device__ __forceinline__ void apply16(double2 (&a)[16], const double2 (&w)[16]) {
+#pragma unroll
+    for (int r = 1; r < 16; ++r) a[r] = cmul(a[r], w[r]);
+}
+
 // w[r] = w1^r, r = 1..7 (depth <= 3)
 __device__ __forceinline__ void powers8(double2 w1, double2 (&w)[8]) {
     w[1] = w1;
@@ -549,6 +567,8 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     int pk_ch = -1;
     float *pk_lds = reinterpret_cast<float *>(twl + kFftTw); // per-wave peaks (fft_peak_stage)
     int pk_pending = -1; // channel whose staged per-wave peaks await thread 0's commit
+    double2 wt[16]; // W_8192^(j c), c = 1..15: built in each final phase, used again by the next stage 1
+    powers16(twl[threadIdx.x], wt);
     int64_t rnd = 0; // round: this workgroup's unit ordinal
     for (int64_t u = fft_unit(0, blockIdx.x, gridDim.x); u < units; u = fft_unit(++rnd, blockIdx.x, gridDim.x)) {
     // Laundered thread index: everything derived from it is recomputed per
@@ -571,7 +591,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
 #pragma unroll
         for (int r = 0; r < 16; ++r) a[r] = make_double2((double)v[r].x, (double)v[r].y);
         dft16(a);
-        twiddle16(a, twl[j]); // W_8192^(b c)
+        apply16(a, wt); // W_8192^(b c): the powers the previous unit's final phase built
         FFT_STAMP(1);
         // No barrier before this write: thread j overwrites exactly the
         // addresses flds[512 c + j] it read itself in the previous unit's
@@ -773,7 +793,8 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     double2 a[16];
 #pragma unroll
     for (int c = 0; c < 16; ++c) a[c] = flds[512 * fft_slot(c) + j];
-    twiddle16(a, twl[j]);
+    powers16(twl[j], wt); // kept for the next unit's stage 1 (same b = j)
+    apply16(a, wt);
     dft16(a);
     FFT_STAMP(13);
     // ---- outputs: c[2m] = Re v'[m], c[2m+1] = -Im v'[m] (conj of the conj
