@@ -641,6 +641,11 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     FFT_STAMP(5);
     // ---- stage B: lane (l1, d1) has gathered l2; radix-8 -> e1; * W_64^(l1 e1)
     powers8(twl[512 + 8 * l1], tws);
+    double2 tws_b[8]; // W_64^(l1 r): stage B' (d1 = lane & 7 = l1) needs the same powers
+    if constexpr (kOut == kFftOutSym) {
+#pragma unroll
+        for (int r = 1; r < 8; ++r) tws_b[r] = tws[r];
+    }
     dft8(x0);
     twiddle8(x0, tws);
 #pragma unroll
@@ -758,7 +763,12 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
         for (int e1 = 0; e1 < 8; ++e1) x0[e1] = blk0[fx3(d1, e1, b0)];
 #pragma unroll
         for (int e1 = 0; e1 < 8; ++e1) x1[e1] = blk1[fx3(d1, e1, b0)];
-        powers8(twl[512 + 8 * d1], tws);
+        if constexpr (kOut == kFftOutSym) {
+#pragma unroll
+            for (int r = 1; r < 8; ++r) tws[r] = tws_b[r]; // registers to spare in this form
+        } else {
+            powers8(twl[512 + 8 * d1], tws);
+        }
         dft8(x0);
         twiddle8(x0, tws);
 #pragma unroll
