@@ -102,7 +102,7 @@ constexpr int kNtStore = 2;
 constexpr int kFftOutF32 = 0, kFftOutFirst = 1, kFftOutAdd = 2, kFftOutLast = 3, kFftOutSym = 4;
 // kFftOutSym = kFftOutF32 for a linear-phase filter in zero-phase form: real
 // pair table (fft_plan_build's symmetric layout), outputs c in [half, L - half)
-constexpr int kFftSymS2 = 0, kFftSymD2 = 8 * kFftNT, kFftSymW = 8 * kFftNT; // doubles, doubles, double2
+constexpr int kFftSymSD = 0, kFftSymW = 8 * kFftNT; // double2 (2S, 2D) per (slot, thread); double2 W of slot 0
 
 // Wave 0, lanes 32..63: the column-0 task pairs (d1A | e1A << 3 | d1B << 6 |
 // e1B << 9), ordered so the exchange-2 reads and exchange-3 writes stay
@@ -663,12 +663,13 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     double qsr[8], qdr[8];                       // kSym: the real 2 S and 2 D
     double2 wbase;                               // W_L^k of slot 0
     if constexpr (kSym) {
-        const double *t = reinterpret_cast<const double *>(pair) + j;
+        const double2 *t = pair + kFftSymSD + j;
         wbase = pair[kFftSymW + j];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            qsr[i] = t[kFftSymS2 + 512 * i];
-            qdr[i] = t[kFftSymD2 + 512 * i];
+            const double2 sd = t[512 * i]; // one 16-byte load per slot
+            qsr[i] = sd.x;
+            qdr[i] = sd.y;
         }
     } else {
         const double2 *t = pair + j;
@@ -1020,9 +1021,7 @@ inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, hipSt
                     pt[(size_t)2 * kFftPairSlots * kFftNT + o] = cplx(c, sn);
                 } else if (i < 8) {
                     // symmetric layout: real 2S, 2D per (slot, thread), W of slot 0
-                    double *pd = reinterpret_cast<double *>(pt);
-                    pd[(size_t)kFftSymS2 + o] = (double)(2 * sr);
-                    pd[(size_t)kFftSymD2 + o] = (double)(2 * dr);
+                    pt[(size_t)kFftSymSD + o] = cplx(2 * sr, 2 * dr);
                     if (i == 0) pt[(size_t)kFftSymW + (size_t)t] = cplx(c, sn);
                 }
                 if (i == 8 && sp) c8[(size_t)part] = cplx(2 * sr - 2 * dr, sym ? 0.0L : 2 * si - 2 * di);
