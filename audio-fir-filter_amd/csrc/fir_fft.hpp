@@ -8,6 +8,9 @@
 //   x_seg[i] = x[n0 - half + i], i in [0, L), L = 16384 real samples
 //   c = IFFT_L( FFT_L(x_seg) * G ),  G = FFT_L(reversed taps, zero padded)
 //   y[n0 + m - (T-1)] = c[m] for m in [T-1, L)          (overlap-save)
+// A linear-phase (symmetric) filter runs in zero-phase form instead
+// (kFftOutSym): G = FFT_L of the taps centred on sample 0 is real, the pair
+// table is real, and y[n0 + m - half] = c[m] for m in [half, L - half).
 // The real length-L transform is one complex M = L/2 = 8192-point FFT of
 // z[m] = x_seg[2m] + i x_seg[2m+1]; the even/odd split and merge are fused
 // with the multiply by G into one "pair" step on bins k and M-k; the inverse
@@ -28,10 +31,11 @@
 //           workgroup-wide transpose and the 16-point DFTs.
 // Per segment: 2 workgroup barriers and 6 LDS round trips of the 128 KiB work
 // array (the radix-16x16x16x2 Stockham form it replaces needed 14 barriers and
-// ~8 round trips).  The grid is persistent (one 512-thread workgroup per CU);
-// samples are read and results written through range-checked raw buffer
-// resources, so the channel-edge zero padding and output clipping need no
-// branches.
+// ~8 round trips).  The grid is persistent (one 512-thread workgroup per CU)
+// and XCD-aware (fft_unit: neighbouring segments on one XCD share their halo
+// in its L2); samples are read and results written (non-temporal) through
+// range-checked raw buffer resources, so the channel-edge zero padding and
+// output clipping need no branches.
 #pragma once
 #include <hip/hip_runtime.h>
 
