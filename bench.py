@@ -13,6 +13,9 @@ a file is split across ranks (or --peak-scope global), then the device-side
 normalize decision and rescale (a no-op unless the peak exceeds 1 or
 --normalize).
 
+  --config 1  1 s mono 48 kHz int16, 19 201 taps (-f 20 -s 10): the reference's
+              CPU-runnable plumbing case; cpu_baseline runs single-threaded, as
+              BASELINE.json states it
   --config 2  (default) one 10-min file per GPU: weak scaling, no collective
   --config 3  one 60-s 8-channel 96 kHz float32 file per GPU, 8001 taps (the
               long-filter stress case; BASELINE.json names no duration, SURVEY.md
@@ -45,7 +48,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
+    ap.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 4, 5])
     ap.add_argument("--method", default="auto", choices=["auto", "direct", "fft"])
     ap.add_argument("--files", type=int, default=None, help="files in the batch (configs 4/5)")
     ap.add_argument("--seconds", type=float, default=None, help="file length in seconds")
@@ -60,7 +63,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     a = ap.parse_args()
-    if a.config == 2:
+    if a.config == 1:
+        a.seconds = 1.0 if a.seconds is None else a.seconds
+        a.channels, a.fs, a.ntaps, a.bits = 1, 48000.0, 19201, 16
+    elif a.config == 2:
         a.seconds = 600.0 if a.seconds is None else a.seconds
     elif a.config == 3:
         a.seconds = 60.0 if a.seconds is None else a.seconds
@@ -90,7 +96,7 @@ def design_taps(ntaps, fs):
     return h
 
 
-def cpu_baseline(x0, taps, budget_s):
+def cpu_baseline(x0, taps, budget_s, max_cores=16):
     """Oracle restatement of the reference threaded CPU path (FilterCore.h +
     ProcessFile.cp:57-87, strict-order double FMA), on a bounded prefix."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -99,7 +105,7 @@ def cpu_baseline(x0, taps, budget_s):
         cores = len(os.sched_getaffinity(0))
     except AttributeError:
         cores = os.cpu_count() or 1
-    cores = max(1, min(cores, 16))  # the box's CPU share for one GPU
+    cores = max(1, min(cores, max_cores))  # the box's CPU share for one GPU
     n_cal = min(x0.size, 16384 * cores)
     t = time.perf_counter()
     oracle.filter_channel_mt(x0[:n_cal], taps, cores, oracle.MODE_FMA)
@@ -190,7 +196,7 @@ def main():
 
     nch, fs = args.channels, args.fs
     n = int(round(args.seconds * fs))
-    per_gpu = args.config in (2, 3)  # one file per rank (weak scaling)
+    per_gpu = args.config in (1, 2, 3)  # one file per rank (weak scaling)
     nfiles = world if per_gpu else args.files
     taps = design_taps(args.ntaps, fs)
     half = (args.ntaps - 1) // 2
@@ -271,7 +277,8 @@ def main():
         simds = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
         fp64_tflops = f64_flops / kern_s / 1e12 if f64_flops else None
         valu_frac = valu_insts * VALU_NS_PER_INST * 1e-9 / (simds * kern_s) if valu_insts else None
-        wl = {2: "config2: 10 min stereo 48 kHz int24 file per GPU",
+        wl = {1: "config1: 1 s mono 48 kHz int16 file per GPU (-f 20 -s 10)",
+              2: "config2: 10 min stereo 48 kHz int24 file per GPU",
               3: f"config3: {args.seconds:g} s 8-channel 96 kHz float32 file per GPU",
               4: f"config4: {nfiles} x {args.seconds / 60:g} min stereo 48 kHz int24 files",
               5: f"config5: {nfiles} x {args.seconds / 60:g} min stereo 48 kHz int24 files, "
@@ -322,7 +329,8 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(file_samples(0).reshape(-1), taps,
-                                                args.cpu_seconds)
+                                                args.cpu_seconds,
+                                                max_cores=1 if args.config == 1 else 16)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
