@@ -118,3 +118,23 @@ def test_normalize_clear_dev(tt):
     with pytest.raises(lc.LcfirError) as e:
         lc.normalize_clear_dev(yb, 5003, 2, 5003, peaks, 3, False, peaks[2:], 1)
     assert "overlap" in str(e.value)
+
+
+def test_normalize_large_buffer(tt):
+    """The rescale loop at full-file sizes (4 loads in flight per thread plus
+    the remainder loop): bit-identical to (float)((double)y * (1 / peak)) on
+    every sample, ragged lengths, a non-16-byte-aligned channel (scalar path)."""
+    torch, lc = tt
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(11)
+    for n, offset in [(3_000_001, 0), (1_048_576 + 5, 0), (2_500_003, 1)]:
+        y0 = (rng.standard_normal((2, n)) * 1.7).astype(np.float32)
+        pk = float(np.abs(y0).max())
+        buf = torch.zeros(2 * n + 8, dtype=torch.float32, device=dev)
+        view = buf[offset:offset + 2 * n].view(2, n)  # offset 1: channel bases 4-byte aligned only
+        view.copy_(torch.from_numpy(y0))
+        peaks = torch.tensor([pk], dtype=torch.float32, device=dev)
+        lc.normalize_dev(view, n, 2, n, peaks, 1, False)
+        torch.cuda.synchronize()
+        ref = (y0.astype(np.float64) * (1.0 / pk)).astype(np.float32)
+        assert np.array_equal(view.cpu().numpy(), ref), (n, offset)
