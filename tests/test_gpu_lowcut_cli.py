@@ -171,3 +171,28 @@ def test_pipeline_stops_at_first_failure(tmp_path):
     assert r.returncode == 1 and "not found" in r.stderr
     assert (outdir / "g0.wav").exists() and (outdir / "g1.wav").exists()
     assert not (outdir / "g2.wav").exists()
+
+
+def test_large_file(tmp_path):
+    """A 42 MB WAVE: every non-payload byte kept, and the payload equal to the
+    same decode -> filter -> encode through the Python binding of the C ABI."""
+    import lcfir as lc
+    rate, nch, n = 48000, 2, 7_000_003
+    x = tone(nch, n, rate)
+    src, dst = tmp_path / "big.wav", tmp_path / "big_out.wav"
+    pcm_ref.write_wave(src, x, rate, "s24le", extra_chunks=[(b"LIST", b"INFOICMT\x04\x00\x00\x00big!")])
+    assert os.path.getsize(src) > (40 << 20)
+    lowcut("-f", 20, "-s", 48, src, dst)
+    a, b = open(src, "rb").read(), open(dst, "rb").read()
+    d = info(src)
+    off, nbytes = int(d["data_offset"]), int(d["data_bytes"])
+    assert len(a) == len(b) and a[:off] == b[:off] and a[off + nbytes:] == b[off + nbytes:]
+    xq = np.ascontiguousarray(pcm_ref.np_decode(a[off:off + nbytes], "s24le", nch), np.float32)
+    flt = lc.Filter(lc.design_lowcut(20.0, 48.0, float(rate)))
+    dx = lc.DeviceBuffer.from_array(xq)
+    dy = lc.DeviceBuffer(xq.nbytes)
+    flt.filter_channels_dev(dx, n, nch, n, dy, n, None)
+    lc.sync()
+    y = dy.download((nch, n))
+    assert np.abs(y).max() <= 1.0  # no normalize in this case
+    assert pcm_ref.np_encode(y, "s24le") == b[off:off + nbytes]

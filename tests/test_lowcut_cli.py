@@ -101,3 +101,13 @@ def test_rejects_unsupported_formats(tmp_path):
     q.write_bytes(b"not audio at all")
     r = run("--info", q)
     assert r.returncode == 1
+
+
+def test_large_file_info(tmp_path):
+    """--info on a 42 MB file (the whole-file read of the container parser)."""
+    n = 7_000_003
+    p = tmp_path / "big.wav"
+    pcm_ref.write_wave(p, sig(2, n, seed=4), 48000, "s24le")
+    assert os.path.getsize(p) > (40 << 20)
+    kind, fmt, f = info(p)
+    assert kind == "WAVE" and fmt == "s24le" and int(f["frames"]) == n and int(f["ch"]) == 2
