@@ -103,17 +103,32 @@ class Backend:
     def new_peaks(self, nfiles: int):
         raise NotImplementedError
 
+    def set_lane(self, lane: int):
+        """issue what follows on pipeline lane `lane` (BatchRunner(lanes > 1))."""
+
+    def join_lanes(self):
+        """every lane's later work follows what lane 0 holds now (the uploads)."""
+
+
 
 class BatchRunner:
     """One rank's share of a batch.  prepare() uploads the rank's sample
     windows (untimed); step() is the timed per-batch compute: filter every
-    shard with fused peaks, exchange peaks if needed, normalize."""
+    shard with fused peaks, exchange peaks if needed, normalize.
+
+    lanes > 1 pipelines consecutive steps: step k is issued on lane k mod
+    lanes (its own stream, output buffers and peak vectors), so on the device
+    a step's first segments run on the CUs the previous step's last round
+    leaves idle.  Steps of one lane stay in order; results() is the latest
+    step's outputs."""
 
     def __init__(self, backend: Backend, rank: int, world: int, nframes: Sequence[int], nch: int,
                  half: int, normalize: bool = False, peak_scope: str = "file",
-                 allreduce_max: Optional[Callable] = None):
+                 allreduce_max: Optional[Callable] = None, lanes: int = 1):
         if peak_scope not in ("file", "global"):
             raise ValueError("peak_scope must be 'file' or 'global'")
+        if lanes < 1:
+            raise ValueError("lanes must be >= 1")
         self.b = backend
         self.rank, self.world = rank, world
         self.nframes = [int(n) for n in nframes]
@@ -129,36 +144,51 @@ class BatchRunner:
         if self.exchange and allreduce_max is None:
             raise ValueError("this plan needs a MAX all-reduce of the peak vector")
         self.allreduce_max = allreduce_max
-        # two peak vectors, alternating by step: a step's last normalize
-        # launch also zeroes the other one for the next step, so no separate
-        # reset launch sits in the step
-        self._peak_bufs = [backend.new_peaks(len(self.nframes)) for _ in range(2)]
-        self._cur = 0
-        self.peaks = self._peak_bufs[0]  # the most recent step's per-file peaks
+        # per lane, two peak vectors alternating by step: a step's last
+        # normalize launch also zeroes the other one for the lane's next step,
+        # so no separate reset launch sits in the step
+        self.lanes = lanes
+        self._peak_bufs = [[backend.new_peaks(len(self.nframes)) for _ in range(2)]
+                           for _ in range(lanes)]
+        self._cur = [0] * lanes
+        self._lane = 0
+        self.peaks = self._peak_bufs[0][0]  # the most recent step's per-file peaks
         self.inputs = []
         self.outputs = []
+        self._outs = [[] for _ in range(lanes)]
 
     def prepare(self, get_window: Callable):
         """get_window(file, x_lo, x_hi) -> [nch][x_hi - x_lo] float32 samples."""
-        self.inputs, self.outputs = [], []
-        for pk in self._peak_bufs:
-            self.b.zero_peaks(pk)
+        self.inputs = []
+        self._outs = [[] for _ in range(self.lanes)]
+        self.b.set_lane(0)
+        for bufs in self._peak_bufs:
+            for pk in bufs:
+                self.b.zero_peaks(pk)
         for sh in self.shards:
             n = self.nframes[sh.file]
             lo, hi = window(sh, n, self.half)
             self.inputs.append((self.b.upload(sh.file, get_window(sh.file, lo, hi), lo, hi), lo, hi))
-            self.outputs.append(self.b.alloc_out(self.nch, sh.end - sh.start))
+            for outs in self._outs:
+                outs.append(self.b.alloc_out(self.nch, sh.end - sh.start))
+        self.outputs = self._outs[0]
+        self.b.join_lanes()
+        self._cur = [0] * self.lanes
+        self._lane = 0
 
     def step(self):
-        peaks = self._peak_bufs[self._cur]      # zero (prepare, or the previous step)
-        nxt = self._peak_bufs[1 - self._cur]
-        for sh, (xw, lo, hi), yw in zip(self.shards, self.inputs, self.outputs):
+        lane = self._lane
+        self.b.set_lane(lane)
+        outputs = self._outs[lane]
+        peaks = self._peak_bufs[lane][self._cur[lane]]      # zero (prepare, or the lane's previous step)
+        nxt = self._peak_bufs[lane][1 - self._cur[lane]]
+        for sh, (xw, lo, hi), yw in zip(self.shards, self.inputs, outputs):
             self.b.filter(xw, lo, hi, self.nframes[sh.file], self.nch, yw, sh.start, sh.end,
                           peaks, sh.file)
         if self.exchange:
             self.allreduce_max(peaks)
         last = len(self.shards) - 1
-        for i, (sh, yw) in enumerate(zip(self.shards, self.outputs)):
+        for i, (sh, yw) in enumerate(zip(self.shards, outputs)):
             slot = None if self.scope == "global" else sh.file
             if i == last:
                 self.b.normalize_clear(yw, self.nch, sh.end - sh.start, peaks, slot, self.normalize,
@@ -168,7 +198,9 @@ class BatchRunner:
         if not self.shards:
             self.b.zero_peaks(nxt)
         self.peaks = peaks
-        self._cur = 1 - self._cur
+        self.outputs = outputs
+        self._cur[lane] = 1 - self._cur[lane]
+        self._lane = (lane + 1) % self.lanes
 
     def results(self):
         """[(shard, output handle)] for this rank."""
@@ -176,14 +208,27 @@ class BatchRunner:
 
 
 class DeviceBackend(Backend):
-    """gfx950 kernels through the C ABI on torch-allocated HBM (one stream)."""
+    """gfx950 kernels through the C ABI on torch-allocated HBM: lane 0 is the
+    caller's current stream, lanes 1.. are streams of their own."""
 
-    def __init__(self, flt, device):
+    def __init__(self, flt, device, lanes: int = 1):
         import torch
         import lcfir
         self.torch, self.lc, self.flt, self.dev = torch, lcfir, flt, device
-        self.stream = torch.cuda.current_stream(device)
+        self.streams = [torch.cuda.current_stream(device)]
+        self.streams += [torch.cuda.Stream(device) for _ in range(lanes - 1)]
+        self.stream = self.streams[0]
         self.sp = self.stream.cuda_stream
+
+    def set_lane(self, lane):
+        s = self.streams[lane]
+        self.stream, self.sp = s, s.cuda_stream
+        # torch-side work of the step (the RCCL peak exchange) follows the lane
+        self.torch.cuda.set_stream(s)
+
+    def join_lanes(self):
+        for s in self.streams[1:]:
+            s.wait_stream(self.streams[0])
 
     def new_peaks(self, nfiles):
         return self.torch.zeros(max(1, nfiles), dtype=self.torch.float32, device=self.dev)

@@ -195,11 +195,16 @@ constexpr int fft_slot_column(int s) { return s == 0 ? 0 : s == 1 ? 8 : s % 2 ==
 // workgroups.  Workgroups are dealt to the 8 XCDs round-robin (b mod 8), so
 // XCD x gets the g/8 consecutive units i g + x g/8 + (b div 8): a segment and
 // its neighbour share the T-1 halo samples, and on one XCD the second read of
-// the halo hits that XCD's L2 instead of HBM.  A bijection on every round, so
-// the last, partial round still covers [i g, units) exactly.
-__host__ __device__ inline int64_t fft_unit(int64_t i, int b, int g) {
-    if (g % 8 != 0) return i * g + b;
-    return i * g + (int64_t)(b % 8) * (g / 8) + b / 8;
+// the halo hits that XCD's L2 instead of HBM.  The last, partial round gives
+// unit i g + b to workgroup b: its units spread over all 8 XCDs, and on each
+// XCD they go to the workgroups dispatched first.  A launch queued behind
+// this one on another stream fills the CUs the tail leaves idle; its own
+// extra-unit workgroups then start early instead of behind the tail.  A
+// bijection on every round, so the last round covers [i g, units) exactly.
+__host__ __device__ inline int64_t fft_unit(int64_t i, int b, int g, int64_t units) {
+    const int64_t base = i * g;
+    if (g % 8 != 0 || base + g > units) return base + b;
+    return base + (int64_t)(b % 8) * (g / 8) + b / 8;
 }
 
 // Task word of thread t = 64 w + lane after exchange 2: task A = (cA, d1A, e1A),
@@ -554,7 +559,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     for (int i = threadIdx.x; i < kFftTw; i += kFftNT) twl[i] = tw[i];
     float2 v[16]; // samples of the unit about to start
     {
-        const int64_t u = fft_unit(0, blockIdx.x, gridDim.x); // < units: the grid is <= units
+        const int64_t u = fft_unit(0, blockIdx.x, gridDim.x, units); // < units: the grid is <= units
         fft_load_unit(p, (int)(u / nseg), p.start + (u % nseg) * B, threadIdx.x, v);
     }
     // vmcnt counts loads and stores together, in issue order, and the wait
@@ -574,7 +579,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     double2 wt[16]; // W_8192^(j c), c = 1..15: built in each final phase, used again by the next stage 1
     powers16(twl[threadIdx.x], wt);
     int64_t rnd = 0; // round: this workgroup's unit ordinal
-    for (int64_t u = fft_unit(0, blockIdx.x, gridDim.x); u < units; u = fft_unit(++rnd, blockIdx.x, gridDim.x)) {
+    for (int64_t u = fft_unit(0, blockIdx.x, gridDim.x, units); u < units; u = fft_unit(++rnd, blockIdx.x, gridDim.x, units)) {
     // Laundered thread index: everything derived from it is recomputed per
     // unit instead of being hoisted out of the loop (keeps pressure down).
     int j = threadIdx.x;
@@ -736,7 +741,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     // Unconditional (the last unit reloads itself): a conditional load would
     // keep the old v live across the whole loop body.
     {
-        const int64_t un1 = fft_unit(rnd + 1, blockIdx.x, gridDim.x);
+        const int64_t un1 = fft_unit(rnd + 1, blockIdx.x, gridDim.x, units);
         const int64_t un = un1 < units ? un1 : u;
         fft_load_unit(p, (int)(un / nseg), p.start + (un % nseg) * B, j, v);
     }

@@ -117,7 +117,7 @@ int main(int argc, char **argv) {
     for (int b = 0; b < grid; ++b) t0 = std::min(t0, tr[b][0]);
     for (int b = 0; b < grid; ++b) {
         int nu = 0;
-        while (lcfir::fft_unit(nu, b, grid) < units) ++nu;
+        while (lcfir::fft_unit(nu, b, grid, units) < units) ++nu;
         if (nu + 1 >= kUtraceSlots) {
             std::fprintf(stderr, "too many units per workgroup for the trace\n");
             return 1;
@@ -150,7 +150,7 @@ int main(int argc, char **argv) {
     double ghz = 0;
     for (int b = 0; b < grid; ++b) {
         int nu = 0;
-        while (lcfir::fft_unit(nu, b, grid) < units) ++nu;
+        while (lcfir::fft_unit(nu, b, grid, units) < units) ++nu;
         ghz += (double)(ck[b][1] - ck[b][0]) / (double)(tr[b][nu + 1] - tr[b][0]) * 0.1;
     }
     std::printf("shader clock (s_memtime / s_memrealtime): %.3f GHz\n", ghz / grid);

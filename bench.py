@@ -58,6 +58,12 @@ def parse():
     ap.add_argument("--bits", type=int, default=24, help="0 = float32 source")
     ap.add_argument("--normalize", action="store_true")
     ap.add_argument("--peak-scope", default="file", choices=["file", "global"])
+    ap.add_argument("--lanes", type=int, default=None,
+                    help="pipeline consecutive steps over this many streams (BatchRunner lanes): "
+                         "a step's first segments fill the CUs the previous step's last round "
+                         "leaves idle; 1 = strictly serial steps.  Default: 2 for the one-file "
+                         "configs 1-3 (+4-5 %% on configs 2/3), 1 for the 8-file configs 4/5 "
+                         "(their 1.3-ms launches gain nothing and two lanes measured -2 %%)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
@@ -75,6 +81,8 @@ def parse():
         a.files = 8 if a.files is None else a.files
         a.seconds = 3600.0 if a.seconds is None else a.seconds
         a.normalize = a.normalize or a.config == 5
+    if a.lanes is None:
+        a.lanes = 2 if a.config in (1, 2, 3) else 1
     return a
 
 
@@ -204,9 +212,9 @@ def main():
     flt = lcfir.Filter(taps, device=local, method=args.method)
     method = flt.method
 
-    backend = TimedBackend(batch.DeviceBackend(flt, dev), torch)
+    backend = TimedBackend(batch.DeviceBackend(flt, dev, lanes=args.lanes), torch)
     runner = batch.BatchRunner(backend, rank, world, [n] * nfiles, nch, half, args.normalize,
-                               args.peak_scope, batch.torch_allreduce_max())
+                               args.peak_scope, batch.torch_allreduce_max(), lanes=args.lanes)
     # synthetic samples; configs 4/5 reuse two generated files to bound host time
     cache = {}
 
@@ -234,6 +242,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     backend.record = False
+    backend.set_lane(0)
     launches = len(backend.events)
     kern_ms = sum(a.elapsed_time(b) for a, b in backend.events) / max(1, launches)
     samples_per_launch = my_samples / max(1, len(runner.shards))
@@ -304,6 +313,7 @@ def main():
                 "parallelism": f"{world} rank(s), files sharded by batch.plan_shards",
                 "normalize": bool(args.normalize), "peak_scope": args.peak_scope,
                 "peak_exchange": runner.exchange,
+                "lanes": args.lanes,
             },
             "roofline": {
                 "bound": "hbm",

@@ -163,3 +163,46 @@ def test_plan_shards_rules():
     p = batch.plan_shards([1001, 10], 3)  # file 0 over ranks 0-1, file 1 on rank 2
     assert [(s[0].file, s[0].start, s[0].end) for s in p] == [(0, 0, 500), (0, 500, 1001), (1, 0, 10)]
     assert batch.window(batch.Shard(0, 500, 1001), 1001, 100) == (400, 1001)
+
+
+class LaneRecorder(OracleBackend):
+    """OracleBackend that records the lane each call is issued on."""
+
+    def __init__(self, taps):
+        super().__init__(taps)
+        self.lane, self.log = 0, []
+
+    def set_lane(self, lane):
+        self.lane = lane
+
+    def filter(self, xw, x_lo, x_hi, n, nch, yw, start, end, peaks, slot):
+        self.log.append(("filter", self.lane, id(yw), id(peaks)))
+        super().filter(xw, x_lo, x_hi, n, nch, yw, start, end, peaks, slot)
+
+
+@pytest.mark.parametrize("lanes,normalize", [(2, True), (3, False)])
+def test_batch_lanes_pipeline(lanes, normalize):
+    """BatchRunner(lanes > 1): step k on lane k mod lanes with that lane's own
+    outputs and peak vectors; every step's results equal the serial reference."""
+    nfiles, nch, n = 2, 2, 3000
+    files = make_files(nfiles, nch, n, True)
+    taps = make_taps()
+    be = LaneRecorder(taps)
+    r = batch.BatchRunner(be, 0, 1, [f.shape[1] for f in files], nch, HALF, normalize, "file",
+                          lanes=lanes)
+    r.prepare(lambda f, lo, hi: files[f][:, lo:hi])
+    ref = reference(nfiles, nch, n, normalize, "file", True)
+    outs_by_lane = {}
+    for k in range(2 * lanes + 1):
+        r.step()
+        res = r.results()
+        for sh, y in res:
+            assert np.array_equal(y, ref[sh.file][:, sh.start:sh.end])
+        step_log = be.log[-nfiles:]
+        assert {lane for _, lane, _, _ in step_log} == {k % lanes}
+        outs_by_lane.setdefault(k % lanes, set()).update(o for _, _, o, _ in step_log)
+    # a lane reuses its own output buffers; lanes never share one
+    assert all(len(v) == nfiles for v in outs_by_lane.values())
+    assert len(set().union(*outs_by_lane.values())) == nfiles * lanes
+    with pytest.raises(ValueError):
+        batch.BatchRunner(be, 0, 1, [n], nch, HALF, lanes=0)

@@ -63,9 +63,11 @@ def test_filter_window_rejects_short_window(tt):
     assert "does not cover" in str(e.value)
 
 
-@pytest.mark.parametrize("normalize,loud", [(False, False), (True, False), (False, True)])
-def test_device_batch_runner(tt, oracle_mod, normalize, loud):
-    """One rank, three files: BatchRunner + DeviceBackend vs ProcessFile.cp:57-101."""
+@pytest.mark.parametrize("normalize,loud,lanes", [(False, False, 1), (True, False, 1), (False, True, 1),
+                                                  (True, True, 2), (False, True, 3)])
+def test_device_batch_runner(tt, oracle_mod, normalize, loud, lanes):
+    """One rank, three files: BatchRunner + DeviceBackend vs ProcessFile.cp:57-101
+    (lanes > 1: consecutive steps pipelined over streams; every step's outputs checked)."""
     torch, lc = tt
     import batch
     import synth
@@ -74,18 +76,26 @@ def test_device_batch_runner(tt, oracle_mod, normalize, loud):
     if loud:
         files[1] = (files[1] * np.float32(3.0)).astype(np.float32)
     flt = lc.Filter(taps, method="direct")
-    r = batch.BatchRunner(batch.DeviceBackend(flt, torch.device("cuda", 0)), 0, 1,
-                          [f.shape[1] for f in files], 2, 400, normalize, "file")
+    be = batch.DeviceBackend(flt, torch.device("cuda", 0), lanes=lanes)
+    r = batch.BatchRunner(be, 0, 1, [f.shape[1] for f in files], 2, 400, normalize, "file",
+                          lanes=lanes)
     r.prepare(lambda f, lo, hi: files[f][:, lo:hi])
-    r.step()
-    r.step()  # steps are repeatable (peaks reset each step)
-    torch.cuda.synchronize()
-    assert not r.exchange
-    for sh, y in r.results():
-        ref = files[sh.file].copy()
-        oracle_mod.process_buffer(ref, taps, nthreads=1, normalize=normalize,
+    refs = {}
+    for f in range(3):
+        refs[f] = files[f].copy()
+        oracle_mod.process_buffer(refs[f], taps, nthreads=1, normalize=normalize,
                                   mode=oracle_mod.MODE_FMA)
-        assert np.array_equal(y.cpu().numpy(), ref[:, sh.start:sh.end])
+    assert not r.exchange
+    steps = []
+    for _ in range(2 * lanes):  # steps are repeatable (peaks reset each step, per lane)
+        r.step()
+        steps.append(r.results())
+    torch.cuda.synchronize()
+    be.set_lane(0)
+    assert len({id(y) for res in steps for _, y in res}) == 3 * lanes  # one output set per lane
+    for res in steps:
+        for sh, y in res:
+            assert np.array_equal(y.cpu().numpy(), refs[sh.file][:, sh.start:sh.end])
 
 
 def test_normalize_clear_dev(tt):
