@@ -1,0 +1,41 @@
+"""bench.py's one-line JSON contract on a short config-2 run (MI355X): the
+keys the driver reads, the roofline and cpu_baseline objects, the parity
+probe within tolerance, for serial and pipelined steps (--lanes 1 / 2)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("lanes", [1, 2])
+def test_bench_json_line(lanes):
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "4", "--warmup", "2",
+           "--seconds", "10", "--cpu-seconds", "1", "--lanes", str(lanes)]
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
+              "roofline", "cpu_baseline", "parity"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 4 and d["warmup"] == 2
+    assert d["value"] > 0 and d["ms_per_step"] > 0 and d["higher_is_better"] is True
+    assert d["config"]["workload"].startswith("config2") and d["config"]["lanes"] == lanes
+    samples = d["config"]["channels"] * d["config"]["samples_per_channel"]
+    assert abs(d["value"] - samples / (d["ms_per_step"] / 1e3) / 1e6) / d["value"] < 0.01
+    r = d["roofline"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in r, k
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-5
+    assert r["kernel"] == "fir_fft_f64_kernel" and r["launches_timed"] == 4
+    cb = d["cpu_baseline"]
+    assert cb["value"] > 0 and cb["kind"] == "port" and cb["cores"] >= 1 and cb["sample"]
+    assert d["parity"]["rms_vs_longdouble"] <= d["parity"]["tol"] == 1e-9
