@@ -201,6 +201,8 @@ class BatchRunner:
         self.outputs = outputs
         self._cur[lane] = 1 - self._cur[lane]
         self._lane = (lane + 1) % self.lanes
+        if lane != 0:
+            self.b.set_lane(0)  # the caller's stream is current again after every step
 
     def results(self):
         """[(shard, output handle)] for this rank."""

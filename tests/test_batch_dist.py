@@ -200,6 +200,7 @@ def test_batch_lanes_pipeline(lanes, normalize):
             assert np.array_equal(y, ref[sh.file][:, sh.start:sh.end])
         step_log = be.log[-nfiles:]
         assert {lane for _, lane, _, _ in step_log} == {k % lanes}
+        assert be.lane == 0  # step() leaves lane 0 (the caller's stream) current
         outs_by_lane.setdefault(k % lanes, set()).update(o for _, _, o, _ in step_log)
     # a lane reuses its own output buffers; lanes never share one
     assert all(len(v) == nfiles for v in outs_by_lane.values())
