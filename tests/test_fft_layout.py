@@ -88,3 +88,24 @@ def test_v5_hazard_detector_is_live():
     lds = NoBarrier()
     sim.v5_forward(np.random.default_rng(1).standard_normal(sim.M) + 0j, lds)
     assert lds.hazards > 0
+
+
+def test_fft_unit_is_a_bijection_per_round(tmp_path):
+    """fft_unit (the persistent grid's unit order) compiled host-only from the
+    header and run here: one-to-one per round, XCD-aware full rounds, identity
+    on the last partial round (tests/cpp/fft_unit_check.hip)."""
+    import shutil
+    import subprocess
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        import pytest
+        pytest.skip("hipcc not available")
+    exe = tmp_path / "fft_unit_check"
+    src = os.path.join(ROOT, "tests", "cpp", "fft_unit_check.hip")
+    subprocess.run([hipcc, "--offload-host-only", "-std=c++17", "-O1",
+                    "-I" + os.path.join(ROOT, "include"),
+                    "-I" + os.path.join(ROOT, "audio-fir-filter_amd", "csrc"), "-o", str(exe), src],
+                   check=True, capture_output=True, timeout=300)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert out.stdout.strip().endswith("errors 0")
