@@ -29,6 +29,7 @@ Prints ONE JSON line on rank 0.
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import sys
@@ -271,16 +272,21 @@ def main():
             rms, npos = parity_probe(x, y.cpu().numpy(), taps)
             del xd, y
         traffic, f64_flops, valu_insts = None, None, None
-        try:
-            with open(args.traffic_json) as f:
-                tj = json.load(f)
+        # the PMC sidecar of this exact launch shape: --traffic-json, else any
+        # profiles/traffic_*.json written for it (scripts/make_traffic_json.py)
+        sidecars = [args.traffic_json] + sorted(glob.glob(os.path.join(ROOT, "profiles", "traffic_*.json")))
+        for path in sidecars:
+            try:
+                with open(path) as f:
+                    tj = json.load(f)
+            except (OSError, ValueError):
+                continue
             if tj.get("method") == method and tj.get("ntaps") == args.ntaps and \
                     tj.get("samples_per_launch") == samples_per_launch:
                 traffic = tj.get("hbm_bytes_per_launch")
                 f64_flops = tj.get("f64_flops_per_launch")
                 valu_insts = tj.get("valu_insts_per_launch")
-        except (OSError, ValueError):
-            pass
+                break
         # The f64 kernels are bound by VALU issue, not HBM: the launch's PMC
         # instruction counts (profiles/traffic_latest.json) over the live kernel time.
         simds = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
