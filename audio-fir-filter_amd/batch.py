@@ -107,7 +107,7 @@ class Backend:
         """issue what follows on pipeline lane `lane` (BatchRunner(lanes > 1))."""
 
     def join_lanes(self):
-        """every lane's later work follows what lane 0 holds now (the uploads)."""
+        """every lane's later work follows everything issued so far on every lane."""
 
 
 
@@ -161,6 +161,7 @@ class BatchRunner:
         """get_window(file, x_lo, x_hi) -> [nch][x_hi - x_lo] float32 samples."""
         self.inputs = []
         self._outs = [[] for _ in range(self.lanes)]
+        self.b.join_lanes()  # a re-prepare waits for steps still in flight on any lane
         self.b.set_lane(0)
         for bufs in self._peak_bufs:
             for pk in bufs:
@@ -229,8 +230,10 @@ class DeviceBackend(Backend):
         self.torch.cuda.set_stream(s)
 
     def join_lanes(self):
-        for s in self.streams[1:]:
-            s.wait_stream(self.streams[0])
+        for s in self.streams:
+            for o in self.streams:
+                if o is not s:
+                    s.wait_stream(o)
 
     def new_peaks(self, nfiles):
         return self.torch.zeros(max(1, nfiles), dtype=self.torch.float32, device=self.dev)

@@ -96,6 +96,16 @@ def test_device_batch_runner(tt, oracle_mod, normalize, loud, lanes):
     for res in steps:
         for sh, y in res:
             assert np.array_equal(y.cpu().numpy(), refs[sh.file][:, sh.start:sh.end])
+    if lanes > 1:
+        # re-prepare straight behind steps still in flight on every lane
+        for _ in range(lanes):
+            r.step()
+        r.prepare(lambda f, lo, hi: files[f][:, lo:hi])
+        r.step()
+        r.step()
+        torch.cuda.synchronize()
+        for sh, y in r.results():
+            assert np.array_equal(y.cpu().numpy(), refs[sh.file][:, sh.start:sh.end])
 
 
 def test_normalize_clear_dev(tt):
