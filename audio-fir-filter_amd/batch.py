@@ -5,7 +5,12 @@ The reference processes the files of a batch strictly one after another
 one process per GPU takes a share of the batch:
 
   * num_files >= world: whole files, round-robin -- "one file per GPU" when
-    num_files == world.  No data-path collective: files are independent.
+    num_files == world.  The filtering needs no collective: files are
+    independent.  With --normalize (config 5) the ranks still MAX all-reduce
+    the [num_files] peak vector (each rank fills its own files' slots, the
+    rest stay 0, so every file keeps its own peak): the step ends with every
+    rank holding the batch's per-file peaks, the RCCL peak exchange
+    BASELINE.json's config 5 names, without changing any file's result.
   * num_files < world: each file is split by sample range over a group of
     ranks (each rank reads its range +- half the kernel, no halo exchange).
     The per-file peak is then the max over the group: that is the one real
@@ -109,6 +114,13 @@ class Backend:
     def join_lanes(self):
         """every lane's later work follows everything issued so far on every lane."""
 
+    def retain(self, handle, lane: int):
+        """`handle` is used by work issued on `lane`: keep its memory alive
+        until that work is done even if the caller drops it first."""
+
+    def publish(self, lane: int):
+        """the caller's current stream waits for everything issued on `lane`."""
+
 
 
 class BatchRunner:
@@ -138,9 +150,11 @@ class BatchRunner:
         self.plan = plan_shards(self.nframes, world)
         self.shards = self.plan[rank]
         split = file_is_split(self.plan)
-        # the collective is needed only where files share ranks, or for the
-        # batch-global variant; per-file peaks of whole files stay local
-        self.exchange = (split or peak_scope == "global") and world > 1
+        # the collective: where files share ranks (a file's peak is the max
+        # over its ranks), for the batch-global variant, and with --normalize
+        # (config 5: every rank learns every file's peak; zeros elsewhere keep
+        # each file's own peak, ProcessFile.cp:92-101)
+        self.exchange = world > 1 and (split or peak_scope == "global" or normalize)
         if self.exchange and allreduce_max is None:
             raise ValueError("this plan needs a MAX all-reduce of the peak vector")
         self.allreduce_max = allreduce_max
@@ -152,6 +166,7 @@ class BatchRunner:
                            for _ in range(lanes)]
         self._cur = [0] * lanes
         self._lane = 0
+        self._last = 0
         self.peaks = self._peak_bufs[0][0]  # the most recent step's per-file peaks
         self.inputs = []
         self.outputs = []
@@ -169,13 +184,20 @@ class BatchRunner:
         for sh in self.shards:
             n = self.nframes[sh.file]
             lo, hi = window(sh, n, self.half)
-            self.inputs.append((self.b.upload(sh.file, get_window(sh.file, lo, hi), lo, hi), lo, hi))
-            for outs in self._outs:
+            xw = self.b.upload(sh.file, get_window(sh.file, lo, hi), lo, hi)
+            self.inputs.append((xw, lo, hi))
+            for lane, outs in enumerate(self._outs):
                 outs.append(self.b.alloc_out(self.nch, sh.end - sh.start))
+                self.b.retain(xw, lane)
+                self.b.retain(outs[-1], lane)
+        for lane, bufs in enumerate(self._peak_bufs):
+            for pk in bufs:
+                self.b.retain(pk, lane)
         self.outputs = self._outs[0]
         self.b.join_lanes()
         self._cur = [0] * self.lanes
         self._lane = 0
+        self._last = 0
 
     def step(self):
         lane = self._lane
@@ -201,13 +223,25 @@ class BatchRunner:
         self.peaks = peaks
         self.outputs = outputs
         self._cur[lane] = 1 - self._cur[lane]
+        self._last = lane
         self._lane = (lane + 1) % self.lanes
         if lane != 0:
             self.b.set_lane(0)  # the caller's stream is current again after every step
 
     def results(self):
-        """[(shard, output handle)] for this rank."""
+        """[(shard, output handle)] of the latest step.  The caller's current
+        stream is made to wait for that step's lane first, so reading the
+        handles there (a copy to the host, a follow-on kernel) needs no
+        device-wide synchronisation."""
+        self.b.publish(self._last)
         return list(zip(self.shards, self.outputs))
+
+    def close(self):
+        """Order every lane's outstanding work before the caller's later work
+        (and before the runner's buffers can be reused)."""
+        self.b.join_lanes()
+        for lane in range(self.lanes):
+            self.b.publish(lane)
 
 
 class DeviceBackend(Backend):
@@ -234,6 +268,16 @@ class DeviceBackend(Backend):
             for o in self.streams:
                 if o is not s:
                     s.wait_stream(o)
+
+    def retain(self, handle, lane):
+        # allocated on the caller's stream, written/read on a side lane: the
+        # caching allocator must not hand the block out again before that
+        # lane's work is done
+        if lane > 0:
+            handle.record_stream(self.streams[lane])
+
+    def publish(self, lane):
+        self.torch.cuda.current_stream(self.dev).wait_stream(self.streams[lane])
 
     def new_peaks(self, nfiles):
         return self.torch.zeros(max(1, nfiles), dtype=self.torch.float32, device=self.dev)

@@ -968,8 +968,9 @@ inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, hipSt
         return false;
     }
     std::vector<double> taps((size_t)ntaps);
-    if (hipMemcpy(taps.data(), d_taps, sizeof(double) * (size_t)ntaps, hipMemcpyDeviceToHost) !=
-        hipSuccess) {
+    if (hipMemcpyAsync(taps.data(), d_taps, sizeof(double) * (size_t)ntaps, hipMemcpyDeviceToHost, s) !=
+            hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
         err = "tap download failed";
         return false;
     }
@@ -1046,21 +1047,23 @@ inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, hipSt
         const long double a = -two_pi * (long double)i / 512.0L;
         tw[(size_t)(512 + i)] = make_double2((double)cosl(a), (double)sinl(a));
     }
-    if (hipMalloc(reinterpret_cast<void **>(&plan.d_pair), sizeof(double2) * pair.size()) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void **>(&plan.d_tw), sizeof(double2) * tw.size()) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void **>(&plan.d_task), sizeof(uint32_t) * task.size()) != hipSuccess) {
-        err = "hipMalloc for the FFT plan failed";
+    // stream-ordered on the ctx's own stream s (freed the same way, fft_plan_free)
+    if (hipMallocAsync(reinterpret_cast<void **>(&plan.d_pair), sizeof(double2) * pair.size(), s) != hipSuccess ||
+        hipMallocAsync(reinterpret_cast<void **>(&plan.d_tw), sizeof(double2) * tw.size(), s) != hipSuccess ||
+        hipMallocAsync(reinterpret_cast<void **>(&plan.d_task), sizeof(uint32_t) * task.size(), s) != hipSuccess) {
+        err = "hipMallocAsync for the FFT plan failed";
         return false;
     }
-    if (hipMemcpy(plan.d_pair, pair.data(), sizeof(double2) * pair.size(), hipMemcpyHostToDevice) !=
+    if (hipMemcpyAsync(plan.d_pair, pair.data(), sizeof(double2) * pair.size(), hipMemcpyHostToDevice, s) !=
             hipSuccess ||
-        hipMemcpy(plan.d_tw, tw.data(), sizeof(double2) * tw.size(), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(plan.d_task, task.data(), sizeof(uint32_t) * task.size(), hipMemcpyHostToDevice) !=
-            hipSuccess) {
+        hipMemcpyAsync(plan.d_tw, tw.data(), sizeof(double2) * tw.size(), hipMemcpyHostToDevice, s) !=
+            hipSuccess ||
+        hipMemcpyAsync(plan.d_task, task.data(), sizeof(uint32_t) * task.size(), hipMemcpyHostToDevice, s) !=
+            hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
         err = "FFT plan upload failed";
         return false;
     }
-    (void)s;
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) == hipSuccess &&
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
@@ -1128,8 +1131,21 @@ inline bool fft_launch_one(const FftPlan &plan, const DirectParams &q, int part,
     return true;
 }
 
+// Partitioned filters (plan.parts > 1) keep f64 partial sums: 2^26 outputs
+// per chunk keep the scratch's byte offsets inside the 32-bit buffer range.
+inline int64_t fft_chunk_outputs(const FftPlan &plan) {
+    return plan.parts == 1 ? fft_chunk() : std::min<int64_t>(fft_chunk(), (int64_t)1 << 26);
+}
+// Doubles of partial-sum scratch one fft_launch of p over nch channels needs
+// (0 for a single-partition filter); the chunks reuse it in stream order.
+inline size_t fft_scratch_doubles(const FftPlan &plan, const DirectParams &p, int nch) {
+    if (plan.parts == 1 || p.end <= p.start) return 0;
+    return (size_t)std::min<int64_t>(p.end - p.start, fft_chunk_outputs(plan)) * (size_t)std::max(nch, 1);
+}
+
 // Filter outputs [p.start, p.end) of nch channels.  p.half / p.ntaps are the
-// filter's own (the plan holds the partitioning).
+// filter's own (the plan holds the partitioning); a partitioned filter needs
+// p.y64 = fft_scratch_doubles() of scratch, owned by the caller's stream.
 inline bool fft_launch(const FftPlan &plan, const DirectParams &p, int nch, hipStream_t s,
                        std::string &err) {
     if (p.end - p.start <= 0 || nch <= 0) return true;
@@ -1137,9 +1153,11 @@ inline bool fft_launch(const FftPlan &plan, const DirectParams &p, int nch, hipS
         err = "too many channels for one launch";
         return false;
     }
-    // partitioned filters keep f64 partial sums: 2^26 outputs keep the
-    // scratch's byte offsets inside the 32-bit buffer range
-    const int64_t chunk = plan.parts == 1 ? fft_chunk() : std::min<int64_t>(fft_chunk(), (int64_t)1 << 26);
+    if (plan.parts > 1 && !p.y64) {
+        err = "partitioned filter without partial-sum scratch";
+        return false;
+    }
+    const int64_t chunk = fft_chunk_outputs(plan);
     for (int64_t cs = p.start; cs < p.end; cs += chunk) {
         DirectParams q = p;
         q.start = cs;
@@ -1157,38 +1175,29 @@ inline bool fft_launch(const FftPlan &plan, const DirectParams &p, int nch, hipS
                 return false;
             continue;
         }
-        const int64_t count = q.end - q.start;
-        double *z = nullptr;
-        hipError_t e = hipMallocAsync(reinterpret_cast<void **>(&z), sizeof(double) * (size_t)(count * nch), s);
-        if (e != hipSuccess) {
-            err = std::string("partial-sum scratch: ") + hipGetErrorString(e);
-            return false;
-        }
-        q.y64 = z;
-        q.y64_stride = count;
-        bool ok = true;
-        for (int part = 0; part < plan.parts && ok; ++part) {
+        // the caller's scratch (p.y64, fft_scratch_doubles): f64 partial sums of
+        // this chunk, element 0 = output q.start
+        q.y64 = p.y64;
+        q.y64_stride = q.end - q.start;
+        for (int part = 0; part < plan.parts; ++part) {
             DirectParams qp = q;
             qp.half = p.half - part * plan.ntaps; // partition part covers taps [part * ntaps, ...)
             qp.peak = part == plan.parts - 1 ? p.peak : nullptr;
+            bool ok;
             if (part == 0) ok = fft_launch_one<kFftOutFirst>(plan, qp, part, nch, s, err);
             else if (part < plan.parts - 1) ok = fft_launch_one<kFftOutAdd>(plan, qp, part, nch, s, err);
             else ok = fft_launch_one<kFftOutLast>(plan, qp, part, nch, s, err);
-        }
-        e = hipFreeAsync(z, s);
-        if (!ok) return false;
-        if (e != hipSuccess) {
-            err = std::string("partial-sum scratch free: ") + hipGetErrorString(e);
-            return false;
+            if (!ok) return false;
         }
     }
     return true;
 }
 
-inline void fft_plan_free(FftPlan &plan) {
-    if (plan.d_pair) (void)hipFree(plan.d_pair);
-    if (plan.d_tw) (void)hipFree(plan.d_tw);
-    if (plan.d_task) (void)hipFree(plan.d_task);
+// stream-ordered on s (the plan was built on it); the caller syncs s
+inline void fft_plan_free(FftPlan &plan, hipStream_t s) {
+    if (plan.d_pair) (void)hipFreeAsync(plan.d_pair, s);
+    if (plan.d_tw) (void)hipFreeAsync(plan.d_tw, s);
+    if (plan.d_task) (void)hipFreeAsync(plan.d_task, s);
     plan = FftPlan{};
 }
 

@@ -21,6 +21,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -38,6 +39,21 @@ struct lcfir_ctx {
     double *d_taps = nullptr;
     lcfir::FftPlan fft; // frequency-domain filter, built lazily
     std::mutex fft_mu;
+    // The ctx's device memory is stream-ordered (hipMallocAsync on `own`), so
+    // destroying a ctx frees it without hipFree's implicit device-wide
+    // synchronisation: lcfir_ctx_destroy waits for the streams in `used` only.
+    hipStream_t own = nullptr;
+    std::mutex streams_mu;
+    std::vector<hipStream_t> used; // every stream a launch of this ctx went to
+    // partitioned FFT filters: f64 partial-sum scratch, one grow-only buffer
+    // per stream (stream order keeps a stream's launches from racing on its own
+    // buffer; different streams never share one)
+    struct Scratch {
+        hipStream_t stream;
+        double *p;
+        size_t cap; // doubles
+    };
+    std::vector<Scratch> scratch;
 };
 
 namespace {
@@ -103,13 +119,43 @@ int resolve_method(lcfir_ctx *ctx) {
     return lcfir::fft_preferred(ctx->ntaps) ? LCFIR_METHOD_FFT : LCFIR_METHOD_DIRECT;
 }
 
-int ensure_fft(lcfir_ctx *ctx, hipStream_t s) {
+int ensure_fft(lcfir_ctx *ctx) {
     std::lock_guard<std::mutex> lk(ctx->fft_mu);
     if (ctx->fft.ready) return LCFIR_OK;
     std::string err;
-    if (!lcfir::fft_plan_build(ctx->fft, ctx->d_taps, ctx->ntaps, s, err))
+    if (!lcfir::fft_plan_build(ctx->fft, ctx->d_taps, ctx->ntaps, ctx->own, err))
         return fail(LCFIR_EDEVICE, "fft plan: %s", err.c_str());
     return LCFIR_OK;
+}
+
+// Remember stream s as one that launched on ctx (lcfir_ctx_destroy waits for it).
+void note_stream(lcfir_ctx *ctx, hipStream_t s) {
+    std::lock_guard<std::mutex> lk(ctx->streams_mu);
+    for (hipStream_t u : ctx->used)
+        if (u == s) return;
+    ctx->used.push_back(s);
+}
+
+// The partial-sum scratch of stream s, at least `need` doubles, allocated and
+// (when it grows) freed in s's own order: no device-wide synchronisation.
+double *stream_scratch(lcfir_ctx *ctx, hipStream_t s, size_t need) {
+    std::lock_guard<std::mutex> lk(ctx->streams_mu);
+    lcfir_ctx::Scratch *slot = nullptr;
+    for (auto &e : ctx->scratch)
+        if (e.stream == s) slot = &e;
+    if (!slot) {
+        ctx->scratch.push_back({s, nullptr, 0});
+        slot = &ctx->scratch.back();
+    }
+    if (slot->cap < need) {
+        if (slot->p) (void)hipFreeAsync(slot->p, s);
+        slot->p = nullptr;
+        slot->cap = 0;
+        if (hipMallocAsync(reinterpret_cast<void **>(&slot->p), need * sizeof(double), s) != hipSuccess)
+            return nullptr;
+        slot->cap = need;
+    }
+    return slot->p;
 }
 
 // Run the filter for outputs [start, end) of nch channels.  x/y geometry as
@@ -118,11 +164,17 @@ int run_filter(lcfir_ctx *ctx, lcfir::DirectParams p, int nch, hipStream_t s) {
     p.taps = ctx->d_taps;
     p.ntaps = ctx->ntaps;
     p.half = ctx->half;
+    note_stream(ctx, s);
     const int m = resolve_method(ctx);
     if (m == LCFIR_METHOD_FFT) {
-        int rc = ensure_fft(ctx, s);
+        int rc = ensure_fft(ctx);
         if (rc) return rc;
         std::string err;
+        if (ctx->fft.parts > 1) {
+            const size_t need = lcfir::fft_scratch_doubles(ctx->fft, p, nch);
+            p.y64 = stream_scratch(ctx, s, need);
+            if (!p.y64) return fail(LCFIR_ENOMEM, "partial-sum scratch of %zu doubles", need);
+        }
         if (!lcfir::fft_launch(ctx->fft, p, nch, s, err))
             return fail(LCFIR_EDEVICE, "fft launch: %s", err.c_str());
         return LCFIR_OK;
@@ -145,12 +197,30 @@ struct Staging {
     size_t y_cap = 0;
 };
 
+// Slots per device: enough streams to keep a GPU busy from host threads (each
+// call is synchronous on its slot), few enough that the reference's default
+// of floor(0.7 * cores) threads per channel (main.cp:75) on a large host does
+// not create a stream per thread.  Callers beyond the cap wait for a slot.
+constexpr int kStagingPerDevice = 16;
+
 std::mutex g_pool_mu;
-std::vector<Staging *> g_pool; // idle slots (process lifetime)
+std::condition_variable g_pool_cv;
+std::vector<Staging *> g_pool;   // idle slots
+std::vector<int> g_pool_live;    // slots in existence, per device
+
+void free_staging(Staging *s) {
+    DeviceGuard g(s->device);
+    if (s->d_x) (void)hipFreeAsync(s->d_x, s->stream);
+    if (s->d_y) (void)hipFreeAsync(s->d_y, s->stream);
+    (void)hipStreamSynchronize(s->stream);
+    (void)hipStreamDestroy(s->stream);
+    delete s;
+}
 
 Staging *borrow_staging(int device) {
-    {
-        std::lock_guard<std::mutex> lk(g_pool_mu);
+    std::unique_lock<std::mutex> lk(g_pool_mu);
+    if ((int)g_pool_live.size() <= device) g_pool_live.resize((size_t)device + 1, 0);
+    for (;;) {
         for (size_t i = 0; i < g_pool.size(); ++i) {
             if (g_pool[i]->device == device) {
                 Staging *s = g_pool[i];
@@ -158,29 +228,40 @@ Staging *borrow_staging(int device) {
                 return s;
             }
         }
+        if (g_pool_live[(size_t)device] < kStagingPerDevice) break;
+        g_pool_cv.wait(lk);
     }
+    ++g_pool_live[(size_t)device];
+    lk.unlock();
     Staging *s = new Staging;
     s->device = device;
     if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
         delete s;
+        std::lock_guard<std::mutex> lk2(g_pool_mu);
+        --g_pool_live[(size_t)device];
+        g_pool_cv.notify_one();
         return nullptr;
     }
     return s;
 }
 
 void return_staging(Staging *s) {
-    std::lock_guard<std::mutex> lk(g_pool_mu);
-    g_pool.push_back(s);
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        g_pool.push_back(s);
+    }
+    g_pool_cv.notify_one();
 }
 
-int grow(float *&buf, size_t &cap, size_t need) {
+// grow-only staging buffer, stream-ordered on the slot's own stream
+int grow(float *&buf, size_t &cap, size_t need, hipStream_t s) {
     if (cap >= need) return LCFIR_OK;
     const size_t want = std::max(need, cap * 2);
-    if (buf) (void)hipFree(buf);
+    if (buf) (void)hipFreeAsync(buf, s);
     buf = nullptr;
     cap = 0;
-    if (hipMalloc(reinterpret_cast<void **>(&buf), want * sizeof(float)) != hipSuccess)
-        return fail(LCFIR_ENOMEM, "hipMalloc(%zu floats) failed", want);
+    if (hipMallocAsync(reinterpret_cast<void **>(&buf), want * sizeof(float), s) != hipSuccess)
+        return fail(LCFIR_ENOMEM, "hipMallocAsync(%zu floats) failed", want);
     cap = want;
     return LCFIR_OK;
 }
@@ -224,16 +305,21 @@ int lcfir_ctx_create(int device, const double *taps, int32_t ntaps, lcfir_ctx **
     ctx->device = device;
     ctx->ntaps = ntaps;
     ctx->half = (ntaps - 1) / 2;
-    if (hipMalloc(reinterpret_cast<void **>(&ctx->d_taps), sizeof(double) * (size_t)ntaps) !=
-        hipSuccess) {
+    if (hipStreamCreateWithFlags(&ctx->own, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;
-        return fail(LCFIR_ENOMEM, "hipMalloc for %d taps failed", ntaps);
+        return fail(LCFIR_EDEVICE, "stream creation failed");
     }
-    if (hipMemcpy(ctx->d_taps, taps, sizeof(double) * (size_t)ntaps, hipMemcpyHostToDevice) !=
-        hipSuccess) {
-        (void)hipFree(ctx->d_taps);
-        delete ctx;
-        return fail(LCFIR_EDEVICE, "tap upload failed");
+    int rc = LCFIR_OK;
+    if (hipMallocAsync(reinterpret_cast<void **>(&ctx->d_taps), sizeof(double) * (size_t)ntaps, ctx->own) !=
+        hipSuccess)
+        rc = fail(LCFIR_ENOMEM, "hipMallocAsync for %d taps failed", ntaps);
+    else if (hipMemcpyAsync(ctx->d_taps, taps, sizeof(double) * (size_t)ntaps, hipMemcpyHostToDevice,
+                            ctx->own) != hipSuccess ||
+             hipStreamSynchronize(ctx->own) != hipSuccess)
+        rc = fail(LCFIR_EDEVICE, "tap upload failed");
+    if (rc) {
+        lcfir_ctx_destroy(ctx);
+        return rc;
     }
     *out = ctx;
     return LCFIR_OK;
@@ -242,9 +328,19 @@ int lcfir_ctx_create(int device, const double *taps, int32_t ntaps, lcfir_ctx **
 int lcfir_ctx_destroy(lcfir_ctx *ctx) {
     if (!ctx) return LCFIR_OK;
     DeviceGuard g(ctx->device);
-    (void)hipDeviceSynchronize();
-    lcfir::fft_plan_free(ctx->fft);
-    if (ctx->d_taps) (void)hipFree(ctx->d_taps);
+    // Wait for the streams this ctx launched on -- not the whole device (the
+    // host-pointer calls have synchronised theirs already; a stream the caller
+    // has destroyed since just reports an error here).  Then every buffer goes
+    // back in `own`'s order, without hipFree's device-wide synchronisation.
+    for (hipStream_t s : ctx->used) (void)hipStreamSynchronize(s);
+    for (auto &e : ctx->scratch)
+        if (e.p) (void)hipFreeAsync(e.p, ctx->own);
+    lcfir::fft_plan_free(ctx->fft, ctx->own);
+    if (ctx->d_taps) (void)hipFreeAsync(ctx->d_taps, ctx->own);
+    if (ctx->own) {
+        (void)hipStreamSynchronize(ctx->own);
+        (void)hipStreamDestroy(ctx->own);
+    }
     delete ctx;
     return LCFIR_OK;
 }
@@ -291,8 +387,8 @@ int lcfir_apply_range(lcfir_ctx *ctx, const float *x, int64_t n, float *y, int64
     if (!g.ok) return fail(LCFIR_EDEVICE, "hipSetDevice(%d) failed", ctx->device);
     Staging *st = borrow_staging(ctx->device);
     if (!st) return fail(LCFIR_EDEVICE, "stream creation failed");
-    int rc = grow(st->d_x, st->x_cap, (size_t)(hi - lo));
-    if (!rc) rc = grow(st->d_y, st->y_cap, (size_t)(end - start));
+    int rc = grow(st->d_x, st->x_cap, (size_t)(hi - lo), st->stream);
+    if (!rc) rc = grow(st->d_y, st->y_cap, (size_t)(end - start), st->stream);
     if (!rc) {
         if (hipMemcpyAsync(st->d_x, x + lo, sizeof(float) * (size_t)(hi - lo),
                            hipMemcpyHostToDevice, st->stream) != hipSuccess)
@@ -324,6 +420,35 @@ int lcfir_apply_range(lcfir_ctx *ctx, const float *x, int64_t n, float *y, int64
     return_staging(st);
     if (!rc && progress) progress(user, (uint64_t)(end - start));
     return rc;
+}
+
+int lcfir_staging_release(int device) {
+    std::vector<Staging *> idle;
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        for (size_t i = 0; i < g_pool.size();) {
+            if (device < 0 || g_pool[i]->device == device) {
+                idle.push_back(g_pool[i]);
+                --g_pool_live[(size_t)g_pool[i]->device];
+                g_pool.erase(g_pool.begin() + (long)i);
+            } else {
+                ++i;
+            }
+        }
+    }
+    g_pool_cv.notify_all();
+    for (Staging *st : idle) free_staging(st);
+    return LCFIR_OK;
+}
+
+int lcfir_staging_count(int device, int *live, int *idle) {
+    if (!live || !idle) return fail(LCFIR_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    *live = (device >= 0 && device < (int)g_pool_live.size()) ? g_pool_live[(size_t)device] : 0;
+    int n = 0;
+    for (Staging *st : g_pool) n += st->device == device;
+    *idle = n;
+    return LCFIR_OK;
 }
 
 int lcfir_apply_range_dev(lcfir_ctx *ctx, const float *d_x, int64_t n, float *d_y, int64_t start,
@@ -470,8 +595,8 @@ int lcfir_channel_peak(int device, const float *y, int64_t n, float *peak) {
     if (!g.ok) return fail(LCFIR_EDEVICE, "hipSetDevice(%d) failed", device);
     Staging *st = borrow_staging(device);
     if (!st) return fail(LCFIR_EDEVICE, "stream creation failed");
-    int rc = grow(st->d_x, st->x_cap, (size_t)n);
-    if (!rc) rc = grow(st->d_y, st->y_cap, 1);
+    int rc = grow(st->d_x, st->x_cap, (size_t)n, st->stream);
+    if (!rc) rc = grow(st->d_y, st->y_cap, 1, st->stream);
     if (!rc && hipMemcpyAsync(st->d_x, y, sizeof(float) * (size_t)n, hipMemcpyHostToDevice,
                               st->stream) != hipSuccess)
         rc = fail(LCFIR_EDEVICE, "H2D copy failed");
@@ -489,8 +614,10 @@ int lcfir_channel_peak(int device, const float *y, int64_t n, float *peak) {
 int lcfir_design_lowcut(double freq_hz, double slope_hz, double fs, double *taps, int32_t cap,
                         int32_t *ntaps) {
     if (!ntaps) return fail(LCFIR_EINVAL, "ntaps is null");
-    if (!(fs > 0.0) || !(slope_hz > 0.0) || !(freq_hz >= 0.0) || !(freq_hz < fs / 2))
-        return fail(LCFIR_EINVAL, "need fs > 0, slope > 0, 0 <= freq < fs/2");
+    // freq 0 would make every low-pass tap 0 and the unity-gain normalisation
+    // 0/0: NaN taps, an all-zero output file (the low-cut of nothing)
+    if (!(fs > 0.0) || !(slope_hz > 0.0) || !(freq_hz > 0.0) || !(freq_hz < fs / 2))
+        return fail(LCFIR_EINVAL, "need fs > 0, slope > 0, 0 < freq < fs/2");
     const long double bw = (long double)slope_hz / (long double)fs;
     const long double half_m = 2.0L / bw; // M / 2
     const long long hm = std::max<long long>(1, llroundl(half_m));
@@ -512,6 +639,8 @@ int lcfir_design_lowcut(double freq_hz, double slope_hz, double fs, double *taps
         h[(size_t)i] = v * w;
         sum += h[(size_t)i];
     }
+    if (!(sum != 0.0L) || !std::isfinite((double)sum))
+        return fail(LCFIR_EINVAL, "low-pass taps sum to %g: no unity-gain normalisation", (double)sum);
     for (int i = 0; i <= M; ++i) h[(size_t)i] = -(h[(size_t)i] / sum); // unity DC gain, inverted
     h[(size_t)half] += 1.0L;                                             // spectral inversion
     for (int i = 0; i <= M; ++i) taps[i] = (double)h[(size_t)i];

@@ -159,6 +159,9 @@ inline void parse_aiff(AudioFile &f, bool aifc) {
             if (aifc && size >= 22) comp.assign(reinterpret_cast<const char *>(&b[body + 18]), 4);
             have_comm = true;
         } else if (id == "SSND") {
+            // offset + blockSize precede the samples; the chunk may run past
+            // EOF (exempt above) but those 8 bytes must be there
+            if (size < 8 || body + 8 > b.size()) throw FormatError("truncated SSND chunk");
             const uint32_t offset = be32(&b[body]);
             f.data_offset = body + 8 + offset;
             have_ssnd = true;

@@ -30,6 +30,7 @@
 #include <map>
 #include <mutex>
 #include <optional>
+#include <set>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -337,6 +338,10 @@ void process_files(const std::vector<std::pair<fs::path, fs::path>> &todo, const
     PinnedPool pool;
     Channel<Job> to_gpu(1), to_writer(2);
     std::thread reader([&] {
+        // outputs scheduled by earlier jobs: the reference's sequential loop
+        // (main.cp:131-146) has written them by the time it checks a later job,
+        // so a repeated destination is "File exists" there too (without -O)
+        std::set<fs::path> scheduled;
         for (size_t i = 0; i < todo.size(); ++i) {
             Job j;
             j.index = i;
@@ -346,8 +351,10 @@ void process_files(const std::vector<std::pair<fs::path, fs::path>> &todo, const
             try {
                 if (!fs::exists(j.in) || !fs::is_regular_file(j.in))
                     throw std::runtime_error("File not found: " + j.in.string());
-                if (fs::exists(j.out) && !o.overwrite)
+                const fs::path canon = fs::weakly_canonical(j.out);
+                if ((fs::exists(j.out) || scheduled.count(canon)) && !o.overwrite)
                     throw std::runtime_error("File exists: " + j.out.string());
+                scheduled.insert(canon);
                 j.f = lcfir_host::read_audio_file(j.in.string(),
                                                   [&](size_t n) { return pool.get(n); });
             } catch (...) {

@@ -55,6 +55,8 @@ _SIGNATURES = {
     "lcfir_ctx_half": ([_ctxp, ctypes.POINTER(_c_i32)], _c_int),
     "lcfir_ctx_ntaps": ([_ctxp, ctypes.POINTER(_c_i32)], _c_int),
     "lcfir_apply_range": ([_ctxp, _vp, _c_i64, _vp, _c_i64, _c_i64, PROGRESS_FN, _vp], _c_int),
+    "lcfir_staging_release": ([_c_int], _c_int),
+    "lcfir_staging_count": ([_c_int, ctypes.POINTER(_c_int), ctypes.POINTER(_c_int)], _c_int),
     "lcfir_apply_range_dev": ([_ctxp, _vp, _c_i64, _vp, _c_i64, _c_i64, _vp], _c_int),
     "lcfir_filter_channels_dev": (
         [_ctxp, _vp, _c_i64, _c_i32, _c_i64, _vp, _c_i64, _vp, _vp], _c_int),
@@ -296,6 +298,18 @@ def filter_channel(channel: np.ndarray, sinc: Filter, num_threads: int,
     if errors:
         raise errors[0]
     return out
+
+
+def staging_release(device: int = -1):
+    """Free the idle staging slots of lcfir_apply_range (-1: every device)."""
+    _check(load().lcfir_staging_release(device))
+
+
+def staging_count(device: int = 0):
+    """(slots in existence, idle slots) of the lcfir_apply_range pool."""
+    live, idle = ctypes.c_int(0), ctypes.c_int(0)
+    _check(load().lcfir_staging_count(device, ctypes.byref(live), ctypes.byref(idle)))
+    return live.value, idle.value
 
 
 # -- device post-pass helpers (ProcessFile.cp:91-101) ---------------------------

@@ -65,6 +65,14 @@ def parse():
                          "leaves idle; 1 = strictly serial steps.  Default: 2 for the one-file "
                          "configs 1-3 (+4-5 %% on configs 2/3), 1 for the 8-file configs 4/5 "
                          "(their 1.3-ms launches gain nothing and two lanes measured -2 %%)")
+    ap.add_argument("--preroll-s", type=float, default=2.0,
+                    help="untimed steps for this many seconds before the --warmup steps: the "
+                         "shader clock ramps over the first few hundred ms of back-to-back "
+                         "launches (DESIGN.md s5), and a 20-step timed region would otherwise "
+                         "sit in that ramp.  0 = off")
+    ap.add_argument("--kernel-launches", type=int, default=20,
+                    help="launches of the filter alone, one stream, after the timed region: "
+                         "the exclusive kernel time roofline.kernel_ms is measured on")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
@@ -130,24 +138,36 @@ def cpu_baseline(x0, taps, budget_s, max_cores=16):
                       f"{dt:.1f} s"}
 
 
-def parity_probe(x, y, taps, k=512):
-    """RMS vs the long-double oracle at sampled positions (rank 0, pre-normalize)."""
+def parity_probe(x, y, taps, start, gain=None, k=512):
+    """RMS and max |error| in f32 ulps vs the long-double oracle at sampled
+    positions of one shard's outputs y = outputs [start, start + y.shape[1]) of
+    the file x (rank 0).  gain: the normalize factor the step applied (None =
+    not rescaled); the oracle value then gets the same f64 rescale and
+    rounding (peak_scale.hpp)."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     rng = np.random.default_rng(5)
     half = (taps.size - 1) // 2
-    sq, cnt = 0.0, 0
+    n = x.shape[1]
+    count = y.shape[1]
+    sq, cnt, worst = 0.0, 0, 0.0
     for c in range(x.shape[0]):
-        n = x.shape[1]
-        idx = np.unique(np.r_[np.arange(0, 64), np.arange(n - 64, n), rng.integers(0, n, k),
+        idx = np.unique(np.r_[np.arange(0, 64), np.arange(count - 64, count), rng.integers(0, count, k),
                               np.arange(half - 8, half + 8)])
-        idx = idx[(idx >= 0) & (idx < n)]
-        ref, _ = oracle.filter_points(x[c], taps, idx, oracle.MODE_LD)
-        d = y[c][idx].astype(np.float64) - ref
+        idx = idx[(idx >= 0) & (idx < count)]
+        ref, _ = oracle.filter_points(x[c], taps, idx + start, oracle.MODE_LD)
+        ref32 = ref.astype(np.float32)
+        if gain is not None:
+            ref32 = (ref32.astype(np.float64) * gain).astype(np.float32)
+            ref = ref32.astype(np.float64)
+        got = y[c][idx]
+        d = got.astype(np.float64) - ref
         sq += float((d * d).sum())
         cnt += idx.size
-    return (sq / cnt) ** 0.5, cnt
+        ulp = np.spacing(np.maximum(np.abs(ref32), np.float32(np.finfo(np.float32).tiny)))
+        worst = max(worst, float((np.abs(d) / ulp.astype(np.float64)).max()))
+    return (sq / cnt) ** 0.5, cnt, worst
 
 
 class TimedBackend:
@@ -228,6 +248,40 @@ def main():
     runner.prepare(lambda f, lo, hi: file_samples(f)[:, lo:hi])
     my_samples = sum(nch * (sh.end - sh.start) for sh in runner.shards)
 
+    # Pre-roll: untimed steps until the shader clock has settled.  Back-to-back
+    # launches ramp it over the first few hundred ms (a 20-step
+    # region right after 5 warmup steps measured 8-20 % below steady state).
+    preroll_steps, t_pre = 0, time.perf_counter()
+    while time.perf_counter() - t_pre < args.preroll_s:
+        for _ in range(8):
+            runner.step()
+        preroll_steps += 8
+        torch.cuda.synchronize(dev)
+    preroll_s = time.perf_counter() - t_pre
+    # The dominant kernel's exclusive time: the same filter launches, one
+    # stream, nothing else in flight (HIP events on that stream), right after
+    # the pre-roll so the clock is the timed steps' clock (measured after the
+    # timed region instead, behind the host-side parity copy, it read ~20 %
+    # long: the clock falls as soon as the GPU idles).  Under two lanes the
+    # timed steps' launches overlap by a tail round, so their start-to-end
+    # events (overlapped_ms) are not one launch's duration.
+    backend.set_lane(0)
+    backend.events = []
+    peaks_scratch = backend.new_peaks(len(runner.nframes))
+    for i in range(2 * args.kernel_launches):
+        backend.record = i >= args.kernel_launches  # the first half: untimed lead-in
+        sh = runner.shards[i % len(runner.shards)] if runner.shards else None
+        if sh is None:
+            break
+        xw, lo, hi = runner.inputs[i % len(runner.shards)]
+        yw = runner._outs[0][i % len(runner.shards)]
+        backend.filter(xw, lo, hi, runner.nframes[sh.file], nch, yw, sh.start, sh.end,
+                       peaks_scratch, sh.file)
+    torch.cuda.synchronize(dev)
+    backend.record = False
+    kern_launches = len(backend.events)
+    kern_ms = sum(a.elapsed_time(b) for a, b in backend.events) / max(1, kern_launches)
+    backend.events = []
     for _ in range(args.warmup):
         runner.step()
     torch.cuda.synchronize(dev)
@@ -245,8 +299,14 @@ def main():
     backend.record = False
     backend.set_lane(0)
     launches = len(backend.events)
-    kern_ms = sum(a.elapsed_time(b) for a, b in backend.events) / max(1, launches)
+    overlapped_ms = sum(a.elapsed_time(b) for a, b in backend.events) / max(1, launches)
     samples_per_launch = my_samples / max(1, len(runner.shards))
+    # parity of the LAST timed step's outputs (rank 0's first shard), copied
+    # out before anything else runs on the device
+    probe = None
+    if rank == 0 and not args.no_parity and runner.shards:
+        sh0, y0 = runner.results()[0]
+        probe = (sh0, y0.cpu().numpy(), float(runner.peaks[sh0.file].item()))
 
     total_samples = torch.tensor([float(my_samples)], dtype=torch.float64, device=dev)
     if world > 1:
@@ -261,16 +321,14 @@ def main():
     direct_tflops = 2.0 * args.ntaps * samples_per_launch / kern_s / 1e12
 
     if rank == 0:
-        rms, npos = None, 0
-        if not args.no_parity and runner.shards:
-            # parity of this rank's first file, recomputed without the normalize pass
-            x = np.ascontiguousarray(file_samples(runner.shards[0].file))
-            xd = torch.from_numpy(x).to(dev)
-            y = torch.empty_like(xd)
-            flt.filter_channels_dev(xd, n, nch, n, y, n, None, torch.cuda.current_stream(dev).cuda_stream)
-            torch.cuda.synchronize(dev)
-            rms, npos = parity_probe(x, y.cpu().numpy(), taps)
-            del xd, y
+        rms, npos, worst_ulp = None, 0, None
+        if probe is not None:
+            sh0, y0, peak0 = probe
+            x = np.ascontiguousarray(file_samples(sh0.file))
+            gain = None
+            if args.normalize or peak0 > 1.0:
+                gain = 1.0 / float(np.float32(peak0))  # the pass's f64 factor (peak_scale.hpp)
+            rms, npos, worst_ulp = parity_probe(x, y0, taps, sh0.start, gain)
         traffic, f64_flops, valu_insts = None, None, None
         # the PMC sidecar of this exact launch shape: --traffic-json, else any
         # profiles/traffic_*.json written for it (scripts/make_traffic_json.py)
@@ -330,7 +388,10 @@ def main():
                 "traffic": traffic,
                 "kernel": "fir_direct_f64_kernel" if method == "direct" else "fir_fft_f64_kernel",
                 "kernel_ms": round(kern_ms, 4),
-                "launches_timed": launches,
+                "kernel_ms_note": f"exclusive: {kern_launches} launches of the filter alone on one "
+                                  f"stream after the timed region (HIP events on that stream)",
+                "launches_timed": kern_launches,
+                "overlapped_kernel_ms": round(overlapped_ms, 4),
                 "bytes_per_unit": 4,
                 "binding": "fp64-valu",
                 "direct_equiv_fp64_tflops": round(direct_tflops, 3),
@@ -341,7 +402,9 @@ def main():
                 "valu_issue_note": "PMC VALU wave-instructions per launch x 2.0 ns / (SIMDs x kernel time); "
                                    "2.0 ns = measured two-wave issue ceiling (tools/valu_rate.hip)",
             },
-            "parity": {"rms_vs_longdouble": rms, "positions": npos, "tol": 1e-9},
+            "parity": {"rms_vs_longdouble": rms, "max_ulp": worst_ulp, "positions": npos,
+                       "tol": 1e-9, "of": "outputs of the last timed step (rank 0, first shard)"},
+            "preroll": {"seconds": round(preroll_s, 3), "steps": preroll_steps},
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(file_samples(0).reshape(-1), taps,

@@ -69,6 +69,9 @@ int lcfir_device_count(int *count);
  * taps = the kernel, ntaps = M + 1 (must be odd), half = getMo2()
  * (FilterCore.h:29). */
 int lcfir_ctx_create(int device, const double *taps, int32_t ntaps, lcfir_ctx **out);
+/* Waits for the streams the ctx launched on (not the whole device) and frees
+ * its device memory in stream order.  The caller must not destroy a stream
+ * that still has work of this ctx queued before calling it. */
 int lcfir_ctx_destroy(lcfir_ctx *ctx);
 int lcfir_ctx_set_method(lcfir_ctx *ctx, int method);
 int lcfir_ctx_get_method(const lcfir_ctx *ctx, int *method);
@@ -86,6 +89,14 @@ int lcfir_ctx_ntaps(const lcfir_ctx *ctx, int32_t *ntaps);
  * done (the reference batches reports every 2048 samples, FilterCore.h:38-54). */
 int lcfir_apply_range(lcfir_ctx *ctx, const float *x, int64_t n, float *y, int64_t start,
                       int64_t end, lcfir_progress_fn progress, void *user);
+/* lcfir_apply_range borrows a staging slot (a HIP stream + grow-only device
+ * buffers) per call from a per-device pool of at most 16 slots; callers beyond
+ * that wait for a free slot, so the reference's default of floor(0.7 cores)
+ * threads per channel (main.cp:75) never creates a stream per thread.
+ * lcfir_staging_release frees the idle slots of `device` (-1: every device);
+ * lcfir_staging_count reports the slots in existence and the idle ones. */
+int lcfir_staging_release(int device);
+int lcfir_staging_count(int device, int *live, int *idle);
 
 /* ---- device-resident variants (async on a hipStream_t passed as void*) -- */
 /* Same as lcfir_apply_range with device pointers; no host synchronisation. */

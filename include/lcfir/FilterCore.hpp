@@ -10,11 +10,19 @@
 //
 // This header provides the same function, same argument meaning, same
 // "void, no throw on the hot path" contract, but evaluated on an MI355X through
-// the C ABI of lcfir.h.  VectorMath and WindowedSinc live in the un-vendored
-// c_lib, so the wrapper is a template over any contiguous float container
-// (std::data / std::size, or .data()/.size()) and any tap container; a
-// WindowedSinc whose taps are not reachable that way specialises
-// lcfir::SincTraits.  ThreadSafeProgress is anything with report(size_t).
+// the C ABI of lcfir.h, as a template over the channel, sinc and progress
+// types (lcfir::apply_filter_range).  The non-template function with the
+// reference's exact parameter types -- the one ProcessFile.cp:71-78 passes by
+// name to std::thread -- is in lcfir/FilterCore.h on top of this one.
+//
+// The wrapper touches its arguments only through what FilterCore.h itself
+// uses: channel.size() / channel.begin() (:28,59,67,74), temp_output[i]
+// (:59,67,74), sinc.getMo2() / sinc.fms(it) (:29,67), progress->report(n)
+// (:44,51) -- plus VectorMath's size constructor (ProcessFile.cp:58).  The
+// taps of a WindowedSinc are read through data()/size() when it has them
+// (or through a lcfir::SincTraits specialisation); otherwise they are recovered
+// exactly from fms() itself: fms over a unit impulse at k is h[k] (every
+// other product is an exact zero), one probe per tap, once per sinc object.
 //
 // Each distinct tap set is uploaded once per process and device (the cache
 // below keys on the tap bytes), as the reference builds its WindowedSinc once
@@ -34,6 +42,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
 #include <utility>
 #include <vector>
 
@@ -98,11 +107,78 @@ private:
 };
 
 // ---- how to reach the taps of a WindowedSinc-like object ---------------------
+// Specialise (data(), size()) for a sinc type whose taps are reachable but not
+// through std::data / std::size.  Without either, the taps are probed with
+// fms() (probe_taps below).
 template <class Sinc, class = void>
 struct SincTraits {
+    static constexpr bool direct = false;
+};
+template <class Sinc>
+struct SincTraits<Sinc, std::void_t<decltype(std::data(std::declval<const Sinc &>())),
+                                    decltype(std::size(std::declval<const Sinc &>()))>> {
+    static constexpr bool direct =
+        std::is_same_v<std::decay_t<decltype(*std::data(std::declval<const Sinc &>()))>, double>;
     static const double *data(const Sinc &s) { return std::data(s); }
     static size_t size(const Sinc &s) { return std::size(s); }
 };
+template <class Sinc, class = void>
+struct sinc_traits_direct : std::false_type {};
+template <class Sinc>
+struct sinc_traits_direct<Sinc, std::enable_if_t<SincTraits<Sinc>::direct>> : std::true_type {};
+
+namespace detail {
+// A channel's samples as a pointer, through the interfaces FilterCore.h uses
+// (begin() for the input, operator[] for the output).
+template <class Channel>
+inline const float *in_ptr(const Channel &c) {
+    return std::size(c) ? &*c.begin() : nullptr;
+}
+template <class Channel>
+inline float *out_ptr(Channel &c) {
+    return std::size(c) ? &c[0] : nullptr;
+}
+
+// Taps of a sinc that exposes only getMo2() and fms(it): T = 2 getMo2() + 1
+// probes of fms over a unit impulse.  fms(p) = sum_k h[k] p[k]; with
+// p = impulse + (T-1-k) every product but h[k] * 1 is an exact zero, so the
+// recovered tap is bit-exact whatever fms's accumulation order.  Cached per
+// sinc object, validated on reuse by getMo2() and one fms() fingerprint over a
+// fixed pseudo-random window (an object rebuilt at the same address with other
+// taps misses).
+template <class Channel, class Sinc>
+std::shared_ptr<const std::vector<double>> probe_taps(const Sinc &sinc) {
+    const int64_t half = (int64_t)sinc.getMo2();
+    if (half < 0 || half > (1 << 24)) throw Error(LCFIR_EINVAL, "sinc.getMo2() out of range");
+    const int64_t T = 2 * half + 1;
+    Channel fp((size_t)T);
+    uint32_t s = 0x9e3779b9u;
+    for (int64_t i = 0; i < T; ++i) {
+        s = s * 1664525u + 1013904223u;
+        fp[(size_t)i] = (float)((int32_t)(s >> 8) - (1 << 23)) * 0x1p-23f;
+    }
+    const double finger = (double)sinc.fms(fp.begin());
+    struct Entry {
+        int64_t half;
+        double finger;
+        std::shared_ptr<const std::vector<double>> taps;
+    };
+    static std::mutex mu;
+    static std::map<const void *, Entry> *cache = new std::map<const void *, Entry>; // never destroyed
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache->find(&sinc);
+    if (it != cache->end() && it->second.half == half &&
+        std::memcmp(&it->second.finger, &finger, sizeof finger) == 0)
+        return it->second.taps;
+    Channel imp((size_t)(2 * T - 1));
+    for (int64_t i = 0; i < 2 * T - 1; ++i) imp[(size_t)i] = 0.0f;
+    imp[(size_t)(T - 1)] = 1.0f;
+    auto taps = std::make_shared<std::vector<double>>((size_t)T);
+    for (int64_t k = 0; k < T; ++k) (*taps)[(size_t)k] = (double)sinc.fms(imp.begin() + (T - 1 - k));
+    (*cache)[&sinc] = Entry{half, finger, taps};
+    return taps;
+}
+} // namespace detail
 
 // ---- per-process filter cache (one upload per tap set and device) -------------
 class FilterCache {
@@ -149,9 +225,15 @@ template <class Channel, class Sinc, class Progress>
 inline void apply_filter_range(const Channel &channel, const Sinc &sinc, Channel &temp_output,
                                int_fast64_t startIdx, int_fast64_t endIdx, Progress *progress) {
     try {
-        auto flt = FilterCache::instance().get(SincTraits<Sinc>::data(sinc),
-                                               SincTraits<Sinc>::size(sinc), default_device());
-        flt->apply_range(std::data(channel), (int64_t)std::size(channel), std::data(temp_output),
+        std::shared_ptr<Filter> flt;
+        if constexpr (sinc_traits_direct<Sinc>::value) {
+            flt = FilterCache::instance().get(SincTraits<Sinc>::data(sinc), SincTraits<Sinc>::size(sinc),
+                                              default_device());
+        } else {
+            const auto taps = detail::probe_taps<Channel>(sinc);
+            flt = FilterCache::instance().get(taps->data(), taps->size(), default_device());
+        }
+        flt->apply_range(detail::in_ptr(channel), (int64_t)std::size(channel), detail::out_ptr(temp_output),
                          (int64_t)startIdx, (int64_t)endIdx, progress);
     } catch (const std::exception &e) {
         last_failure() = e.what();

@@ -86,6 +86,12 @@ def test_design_lowcut_rejects_bad_args():
         lcfir.design_lowcut(20, 0, 48000)
     with pytest.raises(lcfir.LcfirError):
         lcfir.design_lowcut(30000, 10, 48000)
+    # -f 0: every low-pass tap is 0 and the unity-gain normalisation 0/0 --
+    # rejected instead of NaN taps (a silently all-zero output file)
+    with pytest.raises(lcfir.LcfirError, match="freq"):
+        lcfir.design_lowcut(0, 10, 48000)
+    with pytest.raises(lcfir.LcfirError):
+        lcfir.design_lowcut(-5, 10, 48000)
 
 
 def test_header_declares_reference_citations():

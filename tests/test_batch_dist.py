@@ -89,7 +89,7 @@ def _worker(rank, world, port, nfiles, nch, n, normalize, scope, loud, q):
                               HALF, normalize, scope, allreduce)
         r.prepare(lambda f, lo, hi: files[f][:, lo:hi])
         r.step()
-        q.put((rank, r.exchange, [(sh, y.copy()) for sh, y in r.results()]))
+        q.put((rank, r.exchange, [(sh, y.copy()) for sh, y in r.results()], r.peaks.copy()))
     finally:
         dist.destroy_process_group()
 
@@ -131,8 +131,10 @@ def reference(nfiles, nch, n, normalize, scope, loud):
 
 @pytest.mark.parametrize("world,nfiles,normalize,scope,loud,exchange", [
     (2, 2, False, "file", True, False),   # one file per rank: no collective
-    (2, 2, True, "file", False, False),
+    (2, 2, True, "file", False, True),    # whole files + --normalize: per-file peak exchange
+    (2, 2, True, "file", True, True),
     (2, 3, False, "file", True, False),   # 3 files over 2 ranks
+    (2, 3, True, "file", True, True),
     (2, 1, False, "file", True, True),    # one file split over 2 ranks: peak exchange
     (2, 1, True, "file", False, True),
     (3, 2, True, "file", True, True),     # 2 files over 3 ranks (one split)
@@ -143,12 +145,23 @@ def test_batch_matches_serial_reference(world, nfiles, normalize, scope, loud, e
     got = run_dist(world, nfiles, nch, n, normalize, scope, loud)
     ref = reference(nfiles, nch, n, normalize, scope, loud)
     assembled = [np.full_like(r, np.nan) for r in ref]
-    for rank, ex, shards in got:
+    peaks = []
+    for rank, ex, shards, pk in got:
         assert ex == exchange
         for sh, y in shards:
             assembled[sh.file][:, sh.start:sh.end] = y
+        peaks.append(pk)
     for a, r in zip(assembled, ref):
         assert np.array_equal(a, r)
+    if exchange and scope == "file":
+        # after the exchange every rank holds every file's own (pre-normalize) peak
+        files = make_files(nfiles, nch, n, loud)
+        import oracle
+        taps = make_taps()
+        want = np.array([max(float(np.abs(oracle.filter_channel(x[c], taps, oracle.MODE_FMA)).max())
+                             for c in range(nch)) for x in files], np.float32)
+        for pk in peaks:
+            assert np.array_equal(pk, want)
 
 
 def test_plan_shards_rules():

@@ -76,9 +76,59 @@ def test_device_batch_runner(tt, oracle_mod, normalize, loud, lanes):
     if loud:
         files[1] = (files[1] * np.float32(3.0)).astype(np.float32)
     flt = lc.Filter(taps, method="direct")
+    _run_batch_checks(torch, oracle_mod, flt, files, taps, normalize, lanes)
+
+
+def _ulps(a, b):
+    ia = np.asarray(a, np.float32).view(np.int32).astype(np.int64)
+    ib = np.asarray(b, np.float32).view(np.int32).astype(np.int64)
+    ia = np.where(ia < 0, -(ia & 0x7FFFFFFF), ia)
+    ib = np.where(ib < 0, -(ib & 0x7FFFFFFF), ib)
+    return np.abs(ia - ib)
+
+
+@pytest.mark.parametrize("ntaps,lanes,normalize", [(4001, 2, False), (4001, 2, True), (12001, 2, False),
+                                                   (4001, 3, True)])
+def test_device_batch_runner_fft_pipelined(tt, oracle_mod, ntaps, lanes, normalize):
+    """The headline path exactly as bench.py runs it: the FFT kernel (4001 taps;
+    12 001 = two partitions), consecutive steps pipelined over lanes -- every
+    step's outputs, read through results() with NO device synchronisation
+    (results() orders the caller's stream behind the step's lane), against the
+    long-double oracle (<= 1 ulp, RMS <= 1e-9)."""
+    torch, lc = tt
+    import batch
+    import synth
+    taps = oracle_mod.design_lowcut(20.0, 48000.0, ntaps)
+    files = [synth.file_buffer(2, 40000 + 3001 * f, 48000.0, file=f, bits=24) for f in range(3)]
+    files[2] = (files[2] * np.float32(3.0)).astype(np.float32)  # loud: rescaled by 1/peak
+    flt = lc.Filter(taps, method="fft")
+    half = (taps.size - 1) // 2
+    refs = {}
+    for f in range(3):
+        y = np.stack([oracle_mod.filter_channel(files[f][c], taps, oracle_mod.MODE_LD) for c in range(2)])
+        peak = float(np.abs(y).max())
+        if normalize or peak > 1.0:
+            y = (y.astype(np.float64) * (1.0 / peak)).astype(np.float32)
+        refs[f] = y
     be = batch.DeviceBackend(flt, torch.device("cuda", 0), lanes=lanes)
-    r = batch.BatchRunner(be, 0, 1, [f.shape[1] for f in files], 2, 400, normalize, "file",
-                          lanes=lanes)
+    r = batch.BatchRunner(be, 0, 1, [f.shape[1] for f in files], 2, half, normalize, "file", lanes=lanes)
+    r.prepare(lambda f, lo, hi: files[f][:, lo:hi])
+    for k in range(2 * lanes + 1):  # an odd number of steps: the last one on lane 0 ... lanes-1
+        r.step()
+        for sh, y in r.results():
+            got = y.cpu().numpy()  # on the caller's stream, no synchronize()
+            want = refs[sh.file]
+            assert _ulps(got, want).max() <= 1, (k, sh.file)
+            d = got.astype(np.float64) - want
+            assert np.sqrt(np.mean(d * d)) <= RMS_TOL
+    r.close()
+
+
+def _run_batch_checks(torch, oracle_mod, flt, files, taps, normalize, lanes):
+    import batch
+    be = batch.DeviceBackend(flt, torch.device("cuda", 0), lanes=lanes)
+    r = batch.BatchRunner(be, 0, 1, [f.shape[1] for f in files], 2, (taps.size - 1) // 2, normalize,
+                          "file", lanes=lanes)
     r.prepare(lambda f, lo, hi: files[f][:, lo:hi])
     refs = {}
     for f in range(3):

@@ -15,7 +15,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 @pytest.mark.parametrize("lanes", [1, 2])
 def test_bench_json_line(lanes):
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "4", "--warmup", "2",
-           "--seconds", "10", "--cpu-seconds", "1", "--lanes", str(lanes)]
+           "--seconds", "10", "--cpu-seconds", "1", "--lanes", str(lanes), "--preroll-s", "0.2",
+           "--kernel-launches", "5"]
     out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
@@ -35,7 +36,11 @@ def test_bench_json_line(lanes):
         assert k in r, k
     assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-5
-    assert r["kernel"] == "fir_fft_f64_kernel" and r["launches_timed"] == 4
+    assert r["kernel"] == "fir_fft_f64_kernel" and r["launches_timed"] == 5
+    # achieved = algorithmic read bytes of one launch / its exclusive duration
+    assert abs(r["achieved"] - 4 * samples / (r["kernel_ms"] / 1e3) / 1e9) / r["achieved"] < 1e-3
+    assert d["preroll"]["steps"] > 0
     cb = d["cpu_baseline"]
     assert cb["value"] > 0 and cb["kind"] == "port" and cb["cores"] >= 1 and cb["sample"]
     assert d["parity"]["rms_vs_longdouble"] <= d["parity"]["tol"] == 1e-9
+    assert d["parity"]["max_ulp"] <= 1.0

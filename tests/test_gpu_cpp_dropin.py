@@ -44,3 +44,36 @@ def test_cpp_process_buffer(driver, tmp_path, oracle_mod, threads, mode, normali
     d = y.astype(np.float64) - ref
     assert np.sqrt(np.mean(d * d)) <= 1e-9
     assert abs(peak - ref_peak) <= 1e-7 * ref_peak
+
+
+DROPIN = os.path.join(ROOT, "tests", "cpp", "dropin_processfile")
+
+
+@pytest.fixture(scope="module")
+def dropin():
+    subprocess.run(["make", "-C", os.path.dirname(DROPIN)], check=True, capture_output=True)
+    return DROPIN
+
+
+@pytest.mark.parametrize("threads", [1, 3, 8, 64])
+def test_reference_call_shape(dropin, tmp_path, oracle_mod, threads):
+    """ProcessFile.cp:57-87 with apply_filter_range passed by name to std::thread
+    (Diskerror::apply_filter_range of include/lcfir/FilterCore.h, reference
+    parameter types), a WindowedSinc stand-in with only getMo2()/fms(): taps
+    recovered through fms, every chunk a concurrent lcfir_apply_range call."""
+    g = load_golden("random_int24")
+    x, taps = g["x"], g["taps"]
+    xi, ti, yo = tmp_path / "x.f32", tmp_path / "t.f64", tmp_path / "y.f32"
+    np.ascontiguousarray(x, np.float32).tofile(xi)
+    np.ascontiguousarray(taps, np.float64).tofile(ti)
+    r = subprocess.run([dropin, str(xi), str(ti), str(yo), str(x.shape[0]), str(x.shape[1]),
+                        str(threads)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    out = dict(line.split() for line in r.stdout.strip().splitlines())
+    assert int(out["progress"]) == x.size  # every sample reported exactly once
+    y = np.fromfile(yo, np.float32).reshape(x.shape)
+    for c in range(x.shape[0]):
+        ref = oracle_mod.filter_channel(x[c], taps, oracle_mod.MODE_LD)
+        d = y[c].astype(np.float64) - ref
+        assert np.sqrt(np.mean(d * d)) <= 1e-9
+        assert np.all(np.abs(d) <= np.spacing(np.abs(ref).astype(np.float32)).astype(np.float64))

@@ -196,3 +196,26 @@ def test_large_file(tmp_path):
     y = dy.download((nch, n))
     assert np.abs(y).max() <= 1.0  # no normalize in this case
     assert pcm_ref.np_encode(y, "s24le") == b[off:off + nbytes]
+
+
+def test_batch_duplicate_destination(tmp_path):
+    """Two inputs with one file name (dirA/x.wav dirB/x.wav out/): the
+    reference's sequential loop (main.cp:131-146) has written out/x.wav when it
+    reaches the second, so without -O that is "File exists"; with -O the second
+    file's result is the one left."""
+    xs = []
+    for d, seed in (("A", 1), ("B", 2)):
+        (tmp_path / d).mkdir()
+        x = tone(1, 9000 + seed, 48000)
+        pcm_ref.write_wave(tmp_path / d / "x.wav", x, 48000, "s16le")
+        xs.append(tmp_path / d / "x.wav")
+    outdir = tmp_path / "out"
+    args = ["-f", 20, "-s", 48, xs[0], xs[1], outdir]
+    r = subprocess.run([LOWCUT, *map(str, args)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 1 and "exists" in r.stderr
+    assert (outdir / "x.wav").exists()
+    first = open(outdir / "x.wav", "rb").read()
+    lowcut("-O", *args)
+    solo = tmp_path / "solo.wav"
+    lowcut("-f", 20, "-s", 48, xs[1], solo)
+    assert open(outdir / "x.wav", "rb").read() == open(solo, "rb").read() != first

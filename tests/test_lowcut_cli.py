@@ -111,3 +111,16 @@ def test_large_file_info(tmp_path):
     assert os.path.getsize(p) > (40 << 20)
     kind, fmt, f = info(p)
     assert kind == "WAVE" and fmt == "s24le" and int(f["frames"]) == n and int(f["ch"]) == 2
+
+
+@pytest.mark.parametrize("ssnd_body", [b"", b"\x00\x00\x00"])
+def test_truncated_ssnd_header(tmp_path, ssnd_body):
+    """An SSND chunk whose offset/blockSize fields run past EOF is a format
+    error, not a read past the end of the file buffer."""
+    import struct
+    comm = struct.pack(">hIh", 1, 10, 16) + b"\x40\x0e\xbb\x80" + b"\x00" * 6  # 48 kHz
+    body = b"COMM" + struct.pack(">I", len(comm)) + comm + b"SSND" + struct.pack(">I", 8 + 20) + ssnd_body
+    p = tmp_path / "t.aif"
+    p.write_bytes(b"FORM" + struct.pack(">I", 4 + len(body)) + b"AIFF" + body)
+    r = run("--info", p)
+    assert r.returncode == 1 and "SSND" in r.stderr
