@@ -387,11 +387,11 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBPS, 6),
                 "traffic": traffic,
                 "kernel": "fir_direct_f64_kernel" if method == "direct" else "fir_fft_f64_kernel",
-                "kernel_ms": round(kern_ms, 4),
+                "kernel_ms": round(kern_ms, 6),
                 "kernel_ms_note": f"exclusive: {kern_launches} launches of the filter alone on one "
                                   f"stream after the timed region (HIP events on that stream)",
                 "launches_timed": kern_launches,
-                "overlapped_kernel_ms": round(overlapped_ms, 4),
+                "overlapped_kernel_ms": round(overlapped_ms, 6),
                 "bytes_per_unit": 4,
                 "binding": "fp64-valu",
                 "direct_equiv_fp64_tflops": round(direct_tflops, 3),
