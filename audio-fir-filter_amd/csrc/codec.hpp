@@ -94,4 +94,29 @@ __global__ __launch_bounds__(256) void encode_pcm_kernel(const float *__restrict
     }
 }
 
+// encode_pcm_kernel with ProcessFile.cp:91-101's normalize folded in: the
+// per-file decision (peak = max d_peak[0..npeak); rescale iff peak > 1 or
+// force) is read from the device, and each sample is scaled exactly as
+// normalize_kernel does ((float)((double)v * (1.0 / (double)peak))) before
+// it is encoded -- byte-identical to normalize + encode, without the
+// rescale pass's 8 B/sample of HBM traffic.
+__global__ __launch_bounds__(256) void encode_pcm_scaled_kernel(const float *__restrict__ in, int64_t stride,
+                                                               int nch, int64_t frames, PcmFormat f,
+                                                               const unsigned *__restrict__ peak, int npeak,
+                                                               int force, uint8_t *__restrict__ out) {
+    float pk = 0.0f;
+    for (int i = 0; i < npeak; ++i) pk = fmaxf(pk, __uint_as_float(peak[i]));
+    const bool scale = (pk > 1.0f || force) && pk > 0.0f;
+    const double gain = scale ? 1.0 / (double)pk : 1.0;
+    const int64_t total = frames * nch;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t fr = i / nch;
+        const int ch = (int)(i - fr * nch);
+        float v = in[(int64_t)ch * stride + fr];
+        if (scale) v = (float)((double)v * gain);
+        store_bytes(out + i * f.bytes, encode_one(v, f), f.bytes, f.big_endian);
+    }
+}
+
 } // namespace lcfir

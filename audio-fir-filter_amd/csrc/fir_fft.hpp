@@ -134,7 +134,21 @@ struct FftPlan {
     uint32_t *d_task = nullptr; // [512] task words (cA, d1A, e1A, cB, d1B, e1B)
     int cus = 256;             // compute units of the plan's device (persistent grid)
     bool sym = false;          // linear-phase filter run in zero-phase form (kFftOutSym)
+    double2 *d_pair16 = nullptr; // waves16 only: fir_fft16's per-bin (a, b) table, [8][1024]
+    bool waves16 = false;         // sym + LCFIR_FFT_WAVES=16: the 16-wave kernel (fir_fft16.hpp)
 };
+
+// LCFIR_FFT_WAVES=16 runs the zero-phase form on the 16-wave kernel
+// (fir_fft16.hpp: four waves per SIMD).  It is parity-exact but measured
+// 21 % slower on config 2 (+33 % VALU instructions), so this
+// file's 8-wave kernel stays the default.
+inline bool fft_use_w16() {
+    static const bool on = [] {
+        const char *e = std::getenv("LCFIR_FFT_WAVES");
+        return e && std::atoi(e) == 16;
+    }();
+    return on;
+}
 
 // A filter runs in zero-phase form (kFftOutSym: real pair table, a cheaper
 // pair step) when it is one partition, half = (T-1)/2 is even (the output
@@ -924,6 +938,11 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     }
 }
 
+} // namespace lcfir
+
+#include "fir_fft16.hpp"
+
+namespace lcfir {
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
@@ -1038,6 +1057,23 @@ inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, hipSt
             }
         }
     }
+    // fir_fft16's zero-phase table: per bin k = w + 16 (lane + 64 e2) of thread
+    // t = 64 w + lane, slot e2: conj(V_k) = conj(Z_k) a + Z_{M-k} (-i b) with
+    // a = 2S + 2D Im W_L^k, b = 2D Re W_L^k (the P-role form above, valid for
+    // every bin; G is the last partition's spectrum, sym implies one)
+    std::vector<double2> pair16;
+    const bool use16 = sym && fft_use_w16();
+    if (use16) {
+        pair16.resize(kFft16PairTable);
+        for (int t = 0; t < kFft16NT; ++t)
+            for (int e2 = 0; e2 < 8; ++e2) {
+                const int k = (t >> 6) + 16 * ((t & 63) + 64 * e2);
+                const long double gr = re[(size_t)k] * scale, hr = re[(size_t)(kFftM - k)] * scale;
+                const long double sr = gr + hr, dr = gr - hr;
+                const long double a = -two_pi * (long double)k / (long double)kFftL;
+                pair16[(size_t)e2 * kFft16NT + (size_t)t] = cplx(2 * sr + 2 * dr * sinl(a), 2 * dr * cosl(a));
+            }
+    }
     std::vector<double2> tw((size_t)kFftTw);
     for (int i = 0; i < 512; ++i) {
         const long double a = -two_pi * (long double)i / 8192.0L;
@@ -1050,8 +1086,15 @@ inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, hipSt
     // stream-ordered on the ctx's own stream s (freed the same way, fft_plan_free)
     if (hipMallocAsync(reinterpret_cast<void **>(&plan.d_pair), sizeof(double2) * pair.size(), s) != hipSuccess ||
         hipMallocAsync(reinterpret_cast<void **>(&plan.d_tw), sizeof(double2) * tw.size(), s) != hipSuccess ||
-        hipMallocAsync(reinterpret_cast<void **>(&plan.d_task), sizeof(uint32_t) * task.size(), s) != hipSuccess) {
+        hipMallocAsync(reinterpret_cast<void **>(&plan.d_task), sizeof(uint32_t) * task.size(), s) != hipSuccess ||
+        (use16 && hipMallocAsync(reinterpret_cast<void **>(&plan.d_pair16), sizeof(double2) * pair16.size(), s) !=
+                    hipSuccess)) {
         err = "hipMallocAsync for the FFT plan failed";
+        return false;
+    }
+    if (use16 && hipMemcpyAsync(plan.d_pair16, pair16.data(), sizeof(double2) * pair16.size(),
+                              hipMemcpyHostToDevice, s) != hipSuccess) {
+        err = "FFT plan upload failed";
         return false;
     }
     if (hipMemcpyAsync(plan.d_pair, pair.data(), sizeof(double2) * pair.size(), hipMemcpyHostToDevice, s) !=
@@ -1072,6 +1115,7 @@ inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, hipSt
     plan.ntaps = tp;
     plan.parts = parts;
     plan.sym = sym;
+    plan.waves16 = use16;
     plan.B = kFftL - tp + 1;
     plan.c8 = std::move(c8);
     plan.ready = true;
@@ -1131,6 +1175,25 @@ inline bool fft_launch_one(const FftPlan &plan, const DirectParams &q, int part,
     return true;
 }
 
+inline bool fft16_launch(const FftPlan &plan, const DirectParams &q, int nch, hipStream_t s, std::string &err) {
+    static const bool attr = [] {
+        return hipFuncSetAttribute(reinterpret_cast<const void *>(&fir_fft16_f64_kernel<kFftOutSym>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)fft16_lds_bytes()) == hipSuccess;
+    }();
+    (void)attr;
+    const int64_t nseg = (q.end - q.start + plan.B - 1) / plan.B;
+    const int64_t units = nseg * nch;
+    const int64_t grid = std::min<int64_t>(units, (int64_t)plan.cus);
+    hipLaunchKernelGGL(fir_fft16_f64_kernel<kFftOutSym>, dim3((unsigned)grid), dim3(kFft16NT), fft16_lds_bytes(), s, q,
+                       plan.d_pair16, plan.d_tw, plan.B, nseg, units);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        err = hipGetErrorString(e);
+        return false;
+    }
+    return true;
+}
+
 // Partitioned filters (plan.parts > 1) keep f64 partial sums: 2^26 outputs
 // per chunk keep the scratch's byte offsets inside the 32-bit buffer range.
 inline int64_t fft_chunk_outputs(const FftPlan &plan) {
@@ -1170,6 +1233,10 @@ inline bool fft_launch(const FftPlan &plan, const DirectParams &p, int nch, hipS
         q.x_hi = hi;
         q.ntaps = plan.ntaps;
         if (plan.parts == 1) {
+            if (plan.waves16) {
+                if (!fft16_launch(plan, q, nch, s, err)) return false;
+                continue;
+            }
             if (plan.sym ? !fft_launch_one<kFftOutSym>(plan, q, 0, nch, s, err)
                          : !fft_launch_one<kFftOutF32>(plan, q, 0, nch, s, err))
                 return false;
@@ -1198,6 +1265,7 @@ inline void fft_plan_free(FftPlan &plan, hipStream_t s) {
     if (plan.d_pair) (void)hipFreeAsync(plan.d_pair, s);
     if (plan.d_tw) (void)hipFreeAsync(plan.d_tw, s);
     if (plan.d_task) (void)hipFreeAsync(plan.d_task, s);
+    if (plan.d_pair16) (void)hipFreeAsync(plan.d_pair16, s);
     plan = FftPlan{};
 }
 

@@ -374,6 +374,16 @@ int lcfir_ctx_ntaps(const lcfir_ctx *ctx, int32_t *ntaps) {
     return LCFIR_OK;
 }
 
+int lcfir_ctx_fft_waves(lcfir_ctx *ctx, int32_t *waves) {
+    if (!ctx || !waves) return fail(LCFIR_EINVAL, "null argument");
+    *waves = 0;
+    if (!lcfir::fft_supported(ctx->ntaps)) return LCFIR_OK;
+    const int rc = ensure_fft(ctx);
+    if (rc != LCFIR_OK) return rc;
+    *waves = ctx->fft.waves16 ? lcfir::kFft16NT / 64 : lcfir::kFftNT / 64;
+    return LCFIR_OK;
+}
+
 int lcfir_apply_range(lcfir_ctx *ctx, const float *x, int64_t n, float *y, int64_t start,
                       int64_t end, lcfir_progress_fn progress, void *user) {
     if (!ctx || !x || !y) return fail(LCFIR_EINVAL, "null argument");
@@ -695,6 +705,23 @@ int lcfir_encode_pcm_dev(const float *d_in, int64_t in_stride, int32_t nch, int6
     hipLaunchKernelGGL(lcfir::encode_pcm_kernel, dim3(blocks), dim3(256), 0,
                        reinterpret_cast<hipStream_t>(stream), d_in, in_stride, (int)nch, frames,
                        f, reinterpret_cast<uint8_t *>(d_out));
+    LCFIR_HIP(hipGetLastError());
+    return LCFIR_OK;
+}
+
+int lcfir_encode_pcm_scaled_dev(const float *d_in, int64_t in_stride, int32_t nch, int64_t frames, int format,
+                                const float *d_peak, int32_t npeak, int force, void *d_out, void *stream) {
+    lcfir::PcmFormat f;
+    if (!pcm_format(format, f)) return fail(LCFIR_EINVAL, "unknown PCM format %d", format);
+    if (nch < 0 || frames < 0 || npeak < 0) return fail(LCFIR_EINVAL, "negative size");
+    if (nch == 0 || frames == 0) return LCFIR_OK;
+    if (!d_in || !d_out || (npeak > 0 && !d_peak)) return fail(LCFIR_EINVAL, "null argument");
+    if (nch > 1 && in_stride < frames) return fail(LCFIR_EINVAL, "channel stride < frames");
+    const int blocks = stream_blocks(frames * nch, 256 * 8);
+    hipLaunchKernelGGL(lcfir::encode_pcm_scaled_kernel, dim3(blocks), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), d_in, in_stride, (int)nch, frames, f,
+                       reinterpret_cast<const unsigned *>(d_peak), (int)npeak, force ? 1 : 0,
+                       reinterpret_cast<uint8_t *>(d_out));
     LCFIR_HIP(hipGetLastError());
     return LCFIR_OK;
 }

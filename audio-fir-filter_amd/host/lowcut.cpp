@@ -282,7 +282,8 @@ struct Slot {
 
 // Enqueue the whole per-file compute of ProcessFile.cp:40-117 on the slot's
 // stream: H2D raw bytes -> decode/deinterleave -> filter all channels with the
-// peak fused -> device-side normalize decision (:91-101) -> encode -> D2H into
+// peak fused -> encode with the device-side normalize decision and gain
+// folded in (:91-101, :115-117) -> D2H into
 // the same pinned buffer.  Nothing here waits on the device.
 void enqueue_file(Slot &s, Job &j, FilterSet &filters, PinnedPool &pool, const Options &o) {
     const AudioFile &f = j.f;
@@ -305,8 +306,11 @@ void enqueue_file(Slot &s, Job &j, FilterSet &filters, PinnedPool &pool, const O
     check(lcfir_decode_pcm_dev(d_raw, f.pcm_format, nch, n, d_x, n, s.stream), "decode");
     check(lcfir_peak_reset_dev(d_peak, nch, s.stream), "peak reset");
     check(lcfir_filter_channels_dev(flt.ctx, d_x, n, nch, n, d_y, n, d_peak, s.stream), "filter");
-    check(lcfir_normalize_dev(d_y, n, nch, n, d_peak, nch, o.normalize ? 1 : 0, s.stream), "normalize");
-    check(lcfir_encode_pcm_dev(d_y, n, nch, n, f.pcm_format, d_raw, s.stream), "encode");
+    // the normalize decision and gain ride in the encode pass, which reads every
+    // sample anyway: no separate rescale pass over the f32 planes
+    check(lcfir_encode_pcm_scaled_dev(d_y, n, nch, n, f.pcm_format, d_peak, nch, o.normalize ? 1 : 0, d_raw,
+                                      s.stream),
+          "encode");
     check(lcfir_memcpy_d2h_async(f.data + f.data_offset, d_raw, f.data_bytes, s.stream), "d2h");
     check(lcfir_memcpy_d2h_async(s.peaks_host.get(), d_peak, sizeof(float) * (size_t)nch, s.stream),
           "d2h");

@@ -53,6 +53,7 @@ _SIGNATURES = {
     "lcfir_ctx_set_method": ([_ctxp, _c_int], _c_int),
     "lcfir_ctx_get_method": ([_ctxp, ctypes.POINTER(_c_int)], _c_int),
     "lcfir_ctx_half": ([_ctxp, ctypes.POINTER(_c_i32)], _c_int),
+    "lcfir_ctx_fft_waves": ([_ctxp, ctypes.POINTER(_c_i32)], _c_int),
     "lcfir_ctx_ntaps": ([_ctxp, ctypes.POINTER(_c_i32)], _c_int),
     "lcfir_apply_range": ([_ctxp, _vp, _c_i64, _vp, _c_i64, _c_i64, PROGRESS_FN, _vp], _c_int),
     "lcfir_staging_release": ([_c_int], _c_int),
@@ -74,6 +75,8 @@ _SIGNATURES = {
     "lcfir_pcm_bytes": ([_c_int], _c_int),
     "lcfir_decode_pcm_dev": ([_vp, _c_int, _c_i32, _c_i64, _vp, _c_i64, _vp], _c_int),
     "lcfir_encode_pcm_dev": ([_vp, _c_i64, _c_i32, _c_i64, _c_int, _vp, _vp], _c_int),
+    "lcfir_encode_pcm_scaled_dev": ([_vp, _c_i64, _c_i32, _c_i64, _c_int, _vp, _c_i32, _c_int, _vp, _vp],
+                                    _c_int),
     "lcfir_dev_malloc": ([_c_int, ctypes.c_size_t, ctypes.POINTER(_vp)], _c_int),
     "lcfir_dev_free": ([_vp], _c_int),
     "lcfir_memcpy_h2d": ([_vp, _vp, ctypes.c_size_t, _vp], _c_int),
@@ -188,6 +191,13 @@ class Filter:
         return h.value
 
     getMo2 = half
+
+    @property
+    def fft_waves(self) -> int:
+        """Waves per workgroup of the FFT kernel this filter's plan runs (0: no FFT)."""
+        w = ctypes.c_int32()
+        _check(load().lcfir_ctx_fft_waves(self._ctx, ctypes.byref(w)))
+        return w.value
 
     @property
     def ntaps(self) -> int:
@@ -438,3 +448,11 @@ def encode_pcm_dev(d_in, in_stride: int, nch: int, frames: int, fmt: str, d_out,
     """Planar float32 (device) -> interleaved PCM bytes (device)."""
     _check(load().lcfir_encode_pcm_dev(_ptr(d_in), in_stride, nch, frames, PCM_FORMATS[fmt],
                                        _ptr(d_out), stream or None))
+
+
+def encode_pcm_scaled_dev(d_in, in_stride: int, nch: int, frames: int, fmt: str, d_peak, npeak: int,
+                          force: bool, d_out, stream=0):
+    """normalize_dev + encode_pcm_dev in one pass (byte-identical; d_in is not rescaled)."""
+    _check(load().lcfir_encode_pcm_scaled_dev(_ptr(d_in), in_stride, nch, frames, PCM_FORMATS[fmt],
+                                              _ptr(d_peak), npeak, 1 if force else 0, _ptr(d_out),
+                                              stream or None))

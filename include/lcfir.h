@@ -77,6 +77,10 @@ int lcfir_ctx_set_method(lcfir_ctx *ctx, int method);
 int lcfir_ctx_get_method(const lcfir_ctx *ctx, int *method);
 int lcfir_ctx_half(const lcfir_ctx *ctx, int32_t *half); /* getMo2() */
 int lcfir_ctx_ntaps(const lcfir_ctx *ctx, int32_t *ntaps);
+/* Diagnostic: waves per workgroup of the FFT kernel this ctx's plan runs
+ * (8, or 16 for a linear-phase filter under LCFIR_FFT_WAVES=16); builds the
+ * plan if needed.  0 when the tap count is outside the FFT method's range. */
+int lcfir_ctx_fft_waves(lcfir_ctx *ctx, int32_t *waves);
 
 /* ---- the hot path: host-pointer range call ----------------------------- */
 /* Replaces apply_filter_range(channel, sinc, temp_output, startIdx, endIdx,
@@ -181,6 +185,13 @@ int lcfir_decode_pcm_dev(const void *d_in, int format, int32_t nch, int64_t fram
                          float *d_out, int64_t out_stride, void *stream);
 int lcfir_encode_pcm_dev(const float *d_in, int64_t in_stride, int32_t nch, int64_t frames,
                          int format, void *d_out, void *stream);
+/* lcfir_normalize_dev + lcfir_encode_pcm_dev in one pass (ProcessFile.cp:91-101
+ * then :115-117): the normalize decision is taken from d_peak[0..npeak) on the
+ * device and each sample is scaled exactly as lcfir_normalize_dev would scale
+ * it before encoding -- byte-identical output, d_in is left unscaled. */
+int lcfir_encode_pcm_scaled_dev(const float *d_in, int64_t in_stride, int32_t nch, int64_t frames,
+                                int format, const float *d_peak, int32_t npeak, int force,
+                                void *d_out, void *stream);
 
 /* ---- device memory / stream helpers for hosts without a GPU runtime ----- */
 int lcfir_dev_malloc(int device, size_t bytes, void **out);

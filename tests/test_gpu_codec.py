@@ -104,3 +104,28 @@ def test_codec_rejects_bad_format(lc):
     assert lc.load().lcfir_decode_pcm_dev(d.ptr, 99, 1, 4, d.ptr, 4, None) == lc.EINVAL
     assert lc.load().lcfir_encode_pcm_dev(d.ptr, 4, 1, 4, 0, d.ptr, None) == lc.EINVAL
     assert lc.pcm_bytes("s24le") == 3 and lc.load().lcfir_pcm_bytes(0) == 0
+
+
+@pytest.mark.parametrize("fmt", ["s16le", "s24le", "s24be", "f32le"])
+@pytest.mark.parametrize("peak,force", [(0.5, False), (0.5, True), (1.7, False), (0.0, True)])
+def test_encode_scaled_equals_normalize_then_encode(lc, fmt, peak, force):
+    """lcfir_encode_pcm_scaled_dev (the lowcut tool's fused pass) is byte-identical
+    to lcfir_normalize_dev followed by lcfir_encode_pcm_dev (ProcessFile.cp:91-101,
+    :115-117), leaves its input unscaled, and takes the decision from the device."""
+    rng = np.random.default_rng(11)
+    nch, frames = 2, 40003
+    nb = lc.pcm_bytes(fmt)
+    x = (rng.uniform(-1.0, 1.0, (nch, frames)) * max(peak, 1e-3)).astype(np.float32)
+    pk = np.array([peak * 0.75, peak], np.float32)  # per-channel slots, max = peak
+    d_pk = lc.DeviceBuffer.from_array(pk)
+    d_x = lc.DeviceBuffer.from_array(x)
+    d_fused = lc.DeviceBuffer(nb * nch * frames)
+    lc.encode_pcm_scaled_dev(d_x, frames, nch, frames, fmt, d_pk, nch, force, d_fused)
+    d_y = lc.DeviceBuffer.from_array(x)
+    lc.normalize_dev(d_y, frames, nch, frames, d_pk, nch, force)
+    d_ref = lc.DeviceBuffer(nb * nch * frames)
+    lc.encode_pcm_dev(d_y, frames, nch, frames, fmt, d_ref)
+    lc.sync()
+    assert d_fused.download(nb * nch * frames, np.uint8).tobytes() == \
+        d_ref.download(nb * nch * frames, np.uint8).tobytes()
+    assert np.array_equal(d_x.download((nch, frames)), x)
