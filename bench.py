@@ -40,7 +40,9 @@ sys.path.insert(0, os.path.join(ROOT, "audio-fir-filter_amd"))
 
 HBM_PEAK_GBPS = 8000.0      # MI355X_MICROARCH.md:36 (spec)
 FP64_PEAK_TFLOPS = 78.6     # FP64 vector (spec; half the 157.3 TF FP32 vector rate)
-VALU_NS_PER_INST = 2.0      # measured VALU issue ceiling per SIMD, two waves (tools/valu_rate.hip)
+# f64 VALU ceiling per SIMD for the FFT kernel's own instruction mix: 1.71 ns per wave-instruction
+# (tools/valu_mix.hip, 4 waves/SIMD at the 2.4 GHz max clock; profiles/r02_valu_mix.txt)
+VALU_NS_PER_INST = 1.71
 METRIC = "filtered Msamples/sec @4001 taps; achieved HBM GB/s vs roofline"
 
 
@@ -399,8 +401,9 @@ def main():
                 else (round(fp64_tflops / FP64_PEAK_TFLOPS, 4) if fp64_tflops else None),
                 "fp64_tflops_pmc": round(fp64_tflops, 3) if fp64_tflops else None,
                 "valu_issue_frac": round(valu_frac, 4) if valu_frac else None,
-                "valu_issue_note": "PMC VALU wave-instructions per launch x 2.0 ns / (SIMDs x kernel time); "
-                                   "2.0 ns = measured two-wave issue ceiling (tools/valu_rate.hip)",
+                "valu_issue_note": "PMC VALU wave-instructions per launch x 1.71 ns / (SIMDs x kernel time); "
+                                   "1.71 ns = the f64 pipe's measured ceiling for the kernel's own "
+                                   "instruction mix (tools/valu_mix.hip, max clock)",
             },
             "parity": {"rms_vs_longdouble": rms, "max_ulp": worst_ulp, "positions": npos,
                        "tol": 1e-9, "of": "outputs of the last timed step (rank 0, first shard)"},
