@@ -149,6 +149,15 @@ inline bool fft_use_w16() {
     }();
     return on;
 }
+// LCFIR_FFT_WAVES=4: every form on the 4-wave kernel (fir_fft4.hpp: one wave
+// per SIMD, four columns per wave)
+inline bool fft_use_w4() {
+    static const bool on = [] {
+        const char *e = std::getenv("LCFIR_FFT_WAVES");
+        return e && std::atoi(e) == 4;
+    }();
+    return on;
+}
 
 // A filter runs in zero-phase form (kFftOutSym: real pair table, a cheaper
 // pair step) when it is one partition, half = (T-1)/2 is even (the output
@@ -941,6 +950,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
 } // namespace lcfir
 
 #include "fir_fft16.hpp"
+#include "fir_fft4.hpp"
 
 namespace lcfir {
 // ---------------------------------------------------------------------------
@@ -1158,15 +1168,23 @@ inline bool fft_launch_one(const FftPlan &plan, const DirectParams &q, int part,
     static const bool attr = [] {
         return hipFuncSetAttribute(reinterpret_cast<const void *>(&fir_fft_f64_kernel<kOut>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)fft_lds_bytes()) == hipSuccess &&
+               hipFuncSetAttribute(reinterpret_cast<const void *>(&fir_fft4_f64_kernel<kOut>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)fft_lds_bytes()) == hipSuccess;
     }();
     (void)attr;
     const int64_t nseg = (q.end - q.start + plan.B - 1) / plan.B;
     const int64_t units = nseg * nch;
     const int64_t grid = std::min<int64_t>(units, (int64_t)plan.cus * fft_blocks_per_cu());
-    hipLaunchKernelGGL(fir_fft_f64_kernel<kOut>, dim3((unsigned)grid), dim3(kFftNT), fft_lds_bytes(), s, q,
-                       plan.d_pair + (size_t)part * kFftPairTable, plan.d_tw, plan.d_task, plan.B, nseg,
-                       units, plan.c8[(size_t)part]);
+    if (fft_use_w4())
+        hipLaunchKernelGGL(fir_fft4_f64_kernel<kOut>, dim3((unsigned)grid), dim3(kFft4NT), fft_lds_bytes(), s, q,
+                           plan.d_pair + (size_t)part * kFftPairTable, plan.d_tw, plan.d_task, plan.B, nseg,
+                           units, plan.c8[(size_t)part]);
+    else
+        hipLaunchKernelGGL(fir_fft_f64_kernel<kOut>, dim3((unsigned)grid), dim3(kFftNT), fft_lds_bytes(), s, q,
+                           plan.d_pair + (size_t)part * kFftPairTable, plan.d_tw, plan.d_task, plan.B, nseg,
+                           units, plan.c8[(size_t)part]);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         err = hipGetErrorString(e);

@@ -380,7 +380,7 @@ int lcfir_ctx_fft_waves(lcfir_ctx *ctx, int32_t *waves) {
     if (!lcfir::fft_supported(ctx->ntaps)) return LCFIR_OK;
     const int rc = ensure_fft(ctx);
     if (rc != LCFIR_OK) return rc;
-    *waves = ctx->fft.waves16 ? lcfir::kFft16NT / 64 : lcfir::kFftNT / 64;
+    *waves = ctx->fft.waves16 ? lcfir::kFft16NT / 64 : lcfir::fft_use_w4() ? lcfir::kFft4NT / 64 : lcfir::kFftNT / 64;
     return LCFIR_OK;
 }
 

@@ -73,7 +73,7 @@ def parse():
                          "launches (DESIGN.md s5), and a 20-step timed region would otherwise "
                          "sit in that ramp.  0 = off")
     ap.add_argument("--kernel-launches", type=int, default=20,
-                    help="launches of the filter alone, one stream, after the timed region: "
+                    help="launches of the filter alone, one stream, right after the pre-roll: "
                          "the exclusive kernel time roofline.kernel_ms is measured on")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
@@ -391,7 +391,7 @@ def main():
                 "kernel": "fir_direct_f64_kernel" if method == "direct" else "fir_fft_f64_kernel",
                 "kernel_ms": round(kern_ms, 6),
                 "kernel_ms_note": f"exclusive: {kern_launches} launches of the filter alone on one "
-                                  f"stream after the timed region (HIP events on that stream)",
+                                  f"stream right after the pre-roll (HIP events on that stream)",
                 "launches_timed": kern_launches,
                 "overlapped_kernel_ms": round(overlapped_ms, 6),
                 "bytes_per_unit": 4,

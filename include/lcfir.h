@@ -78,8 +78,9 @@ int lcfir_ctx_get_method(const lcfir_ctx *ctx, int *method);
 int lcfir_ctx_half(const lcfir_ctx *ctx, int32_t *half); /* getMo2() */
 int lcfir_ctx_ntaps(const lcfir_ctx *ctx, int32_t *ntaps);
 /* Diagnostic: waves per workgroup of the FFT kernel this ctx's plan runs
- * (8, or 16 for a linear-phase filter under LCFIR_FFT_WAVES=16); builds the
- * plan if needed.  0 when the tap count is outside the FFT method's range. */
+ * (8; 16 for a linear-phase filter under LCFIR_FFT_WAVES=16; 4 under
+ * LCFIR_FFT_WAVES=4); builds the plan if needed.  0 when the tap count is
+ * outside the FFT method's range. */
 int lcfir_ctx_fft_waves(lcfir_ctx *ctx, int32_t *waves);
 
 /* ---- the hot path: host-pointer range call ----------------------------- */
