@@ -19,7 +19,7 @@ step() { # name timeout cmd...
     if [ $rc -ne 0 ]; then echo "!! $name failed rc=$rc"; tail -40 "$OUT/$name.log"; exit $rc; fi
 }
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step pytest_gpu 1200 python -m pytest tests -m gpu -x -q
+step pytest_gpu 1200 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
 step bench 600 python bench.py "$@"
 cd /tmp && export TMPDIR=/tmp
 step rocprof 600 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof_$TAG" -o bench -- \
