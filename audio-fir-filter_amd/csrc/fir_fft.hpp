@@ -229,6 +229,37 @@ __host__ __device__ inline int64_t fft_unit(int64_t i, int b, int g, int64_t uni
     if (g % 8 != 0 || base + g > units) return base + b;
     return base + (int64_t)(b % 8) * (g / 8) + b / 8;
 }
+// the same map in 32-bit arithmetic (fft_launch keeps every launch's units < 2^31)
+__host__ __device__ inline int fft_unit32(int i, int b, int g, int units) {
+    const int base = i * g;
+    if (g % 8 != 0 || base + g > units) return base + b;
+    return base + (b % 8) * (g / 8) + b / 8;
+}
+
+// A launch's unit grid: nch x nseg (channel, segment) units, units < 2^31.
+// The kernels split a unit index into (channel, segment) with a multiply and
+// a shift instead of a division: m = ceil(2^(31+l) / nseg), l = ceil(log2
+// nseg), gives u / nseg = (u m) >> (31 + l) exactly for every u < 2^31 (the
+// round-up method; m < 2^32).  The 64-bit division it replaces expanded to
+// ~130 scalar instructions, twice per segment, and spilled SGPRs.
+struct FftGrid {
+    int32_t nseg;  // segments per channel
+    int32_t units; // channels x nseg
+    uint32_t m;    // ceil(2^(31+l) / nseg)
+    uint32_t sh;   // 31 + l
+};
+inline FftGrid fft_grid(int64_t nseg, int64_t units) {
+    FftGrid g{(int32_t)nseg, (int32_t)units, 0u, 31u};
+    uint32_t l = 0;
+    while (((int64_t)1 << l) < nseg) ++l;
+    const uint64_t num = (uint64_t)1 << (31 + l);
+    g.m = (uint32_t)((num + (uint64_t)nseg - 1) / (uint64_t)nseg);
+    g.sh = 31 + l;
+    return g;
+}
+__host__ __device__ inline int fft_div(int u, const FftGrid &g) {
+    return (int)(((uint64_t)(uint32_t)u * g.m) >> g.sh);
+}
 
 // Task word of thread t = 64 w + lane after exchange 2: task A = (cA, d1A, e1A),
 // task B = (cB, d1B, e1B); bins k = c + 16 (d1 + 8 e1 + 64 e2), e2 = register.
@@ -304,24 +335,61 @@ __device__ __forceinline__ double2 w16(double2 a) {
     else static_assert(m == 0, "unused twiddle");
 }
 
+// The W8^1 = (1-i)/sqrt2 and W8^3 = -(1+i)/sqrt2 rotations leave their sqrt(1/2)
+// factor pending (u1 = sqrt2 a W8^1, u3 = sqrt2 a W8^3: adds only), and the
+// butterfly that consumes them folds it into FMAs.
+__device__ __forceinline__ double2 rot8_1(double2 a) { return make_double2(a.x + a.y, a.y - a.x); }
+__device__ __forceinline__ double2 rot8_3(double2 a) { return make_double2(a.y - a.x, -(a.x + a.y)); }
+// t0 + kR2 u, t0 - kR2 u
+__device__ __forceinline__ void fma_pm(double2 t0, double2 u, double2 &p, double2 &m) {
+    p = make_double2(__builtin_fma(kR2, u.x, t0.x), __builtin_fma(kR2, u.y, t0.y));
+    m = make_double2(__builtin_fma(-kR2, u.x, t0.x), __builtin_fma(-kR2, u.y, t0.y));
+}
+// dft4(a0, a1, a2, a3) for a1 = kR2 u1, a3 = kR2 u3 (sqrt(1/2) pending on both odd inputs)
+__device__ __forceinline__ void dft4_r13(double2 &a0, double2 u1, double2 &a2, double2 u3, double2 &o1,
+                                         double2 &o3) {
+    const double2 t0 = cadd(a0, a2), t1 = csub(a0, a2);
+    const double2 s = cadd(u1, u3), d = csub(u1, u3);
+    // t2 = kR2 s, t3 = -i kR2 d
+    fma_pm(t0, s, a0, a2);
+    o1 = make_double2(__builtin_fma(kR2, d.y, t1.x), __builtin_fma(-kR2, d.x, t1.y));
+    o3 = make_double2(__builtin_fma(-kR2, d.y, t1.x), __builtin_fma(kR2, d.x, t1.y));
+}
+// dft4(a0, a1, a2, a3) for a2 = kR2 u2 (sqrt(1/2) pending on input 2)
+__device__ __forceinline__ void dft4_r2(double2 &a0, double2 &a1, double2 u2, double2 &a2, double2 &a3) {
+    double2 t0, t1;
+    fma_pm(a0, u2, t0, t1);
+    const double2 t2 = cadd(a1, a3), t3 = mul_mi(csub(a1, a3));
+    a0 = cadd(t0, t2);
+    a2 = csub(t0, t2);
+    a1 = cadd(t1, t3);
+    a3 = csub(t1, t3);
+}
+
 // forward 16-point DFT, natural order in and out (4 x 4 Cooley-Tukey)
 __device__ __forceinline__ void dft16(double2 (&a)[16]) {
     // radix-4 over n1 for each n2: slot 4*n1 + n2 -> slot 4*k1 + n2
 #pragma unroll
     for (int n2 = 0; n2 < 4; ++n2) dft4(a[n2], a[4 + n2], a[8 + n2], a[12 + n2]);
-    // twiddles W16^(n2*k1), slot 4*k1 + n2
+    // twiddles W16^(n2*k1), slot 4*k1 + n2, then radix-4 over n2 for each k1:
+    // slot 4*k1 + k2 holds X[k1 + 4*k2].  The W16^2 = W8^1 and W16^6 = W8^3
+    // rotations keep their sqrt(1/2) pending into the radix-4 (dft4_r13 and
+    // the inline forms for rows 1 and 3).
     a[5] = w16<1>(a[5]);
-    a[6] = w16<2>(a[6]);
     a[7] = w16<3>(a[7]);
-    a[9] = w16<2>(a[9]);
     a[10] = w16<4>(a[10]);
-    a[11] = w16<6>(a[11]);
     a[13] = w16<3>(a[13]);
-    a[14] = w16<6>(a[14]);
     a[15] = w16<9>(a[15]);
-    // radix-4 over n2 for each k1: slot 4*k1 + k2 holds X[k1 + 4*k2]
-#pragma unroll
-    for (int k1 = 0; k1 < 4; ++k1) dft4(a[4 * k1], a[4 * k1 + 1], a[4 * k1 + 2], a[4 * k1 + 3]);
+    dft4(a[0], a[1], a[2], a[3]);
+    dft4_r2(a[4], a[5], rot8_1(a[6]), a[6], a[7]); // row 1: (a4, a5 w1, kR2 rot8_1(a6), a7 w3)
+    {
+        // row 2: (a8, kR2 rot8_1(a9), -i a10, kR2 rot8_3(a11))
+        double2 o1, o3;
+        dft4_r13(a[8], rot8_1(a[9]), a[10], rot8_3(a[11]), o1, o3);
+        a[9] = o1;
+        a[11] = o3;
+    }
+    dft4_r2(a[12], a[13], rot8_3(a[14]), a[14], a[15]); // row 3: (a12, a13 w3, kR2 rot8_3(a14), a15 w9)
     double2 t[16];
 #pragma unroll
     for (int k1 = 0; k1 < 4; ++k1)
@@ -340,11 +408,10 @@ __device__ __forceinline__ void dft8(double2 (&a)[8]) {
         b[k] = cadd(a[k], a[k + 4]);
         b[k + 4] = csub(a[k], a[k + 4]);
     }
-    b[5] = w16<2>(b[5]); // W8^1
     b[6] = mul_mi(b[6]); // W8^2
-    b[7] = w16<6>(b[7]); // W8^3
     dft4(b[0], b[1], b[2], b[3]);
-    dft4(b[4], b[5], b[6], b[7]);
+    // (b4, b5 W8^1, b6, b7 W8^3) with the sqrt(1/2) of W8^1 and W8^3 folded into FMAs
+    dft4_r13(b[4], rot8_1(b[5]), b[6], rot8_3(b[7]), b[5], b[7]);
     a[0] = b[0];
     a[2] = b[1];
     a[4] = b[2];
@@ -575,15 +642,16 @@ template <int kOut>
 __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, const double2 *__restrict__ pair,
                                                             const double2 *__restrict__ tw,
                                                             const uint32_t *__restrict__ task, int B,
-                                                            int64_t nseg, int64_t units, double2 c8) {
+                                                            FftGrid gd, double2 c8) {
     extern __shared__ double2 flds[];
     FFT_USTAMP(0);
     double2 *twl = flds + kFftM; // the kFftTw twiddles, LDS-resident
     for (int i = threadIdx.x; i < kFftTw; i += kFftNT) twl[i] = tw[i];
     float2 v[16]; // samples of the unit about to start
     {
-        const int64_t u = fft_unit(0, blockIdx.x, gridDim.x, units); // < units: the grid is <= units
-        fft_load_unit(p, (int)(u / nseg), p.start + (u % nseg) * B, threadIdx.x, v);
+        const int u = fft_unit32(0, blockIdx.x, gridDim.x, gd.units); // < units: the grid is <= units
+        const int c = fft_div(u, gd);
+        fft_load_unit(p, c, p.start + (int64_t)(u - c * gd.nseg) * B, threadIdx.x, v);
     }
     // vmcnt counts loads and stores together, in issue order, and the wait
     // pass merges the loop's entry and back edge path-insensitively.  Both
@@ -601,8 +669,9 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     int pk_pending = -1; // channel whose staged per-wave peaks await thread 0's commit
     double2 wt[16]; // W_8192^(j c), c = 1..15: built in each final phase, used again by the next stage 1
     powers16(twl[threadIdx.x], wt);
-    int64_t rnd = 0; // round: this workgroup's unit ordinal
-    for (int64_t u = fft_unit(0, blockIdx.x, gridDim.x, units); u < units; u = fft_unit(++rnd, blockIdx.x, gridDim.x, units)) {
+    int rnd = 0; // round: this workgroup's unit ordinal
+    for (int u = fft_unit32(0, blockIdx.x, gridDim.x, gd.units); u < gd.units;
+         u = fft_unit32(++rnd, blockIdx.x, gridDim.x, gd.units)) {
     // Laundered thread index: everything derived from it is recomputed per
     // unit instead of being hoisted out of the loop (keeps pressure down).
     int j = threadIdx.x;
@@ -612,8 +681,8 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     // the wave's two columns {w, 16 - w} (wave 0: {0, 8}) in adjacent slots
     double2 *blk0 = flds + 512 * (2 * w);
     double2 *blk1 = blk0 + 512;
-    const int ch = (int)(u / nseg);
-    const int64_t n0 = p.start + (u % nseg) * B;
+    const int ch = fft_div(u, gd);
+    const int64_t n0 = p.start + (int64_t)(u - ch * gd.nseg) * B;
     FFT_STAMP(0);
     FFT_USTAMP(1 + rnd);
 
@@ -764,9 +833,10 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     // Unconditional (the last unit reloads itself): a conditional load would
     // keep the old v live across the whole loop body.
     {
-        const int64_t un1 = fft_unit(rnd + 1, blockIdx.x, gridDim.x, units);
-        const int64_t un = un1 < units ? un1 : u;
-        fft_load_unit(p, (int)(un / nseg), p.start + (un % nseg) * B, j, v);
+        const int un1 = fft_unit32(rnd + 1, blockIdx.x, gridDim.x, gd.units);
+        const int un = un1 < gd.units ? un1 : u;
+        const int cn = fft_div(un, gd);
+        fft_load_unit(p, cn, p.start + (int64_t)(un - cn * gd.nseg) * B, j, v);
     }
 
     // ---- inverse stage A': per task radix-8 over e2 -> beta0; * W_512^(beta0 d')
@@ -1175,16 +1245,17 @@ inline bool fft_launch_one(const FftPlan &plan, const DirectParams &q, int part,
     }();
     (void)attr;
     const int64_t nseg = (q.end - q.start + plan.B - 1) / plan.B;
-    const int64_t units = nseg * nch;
+    const int64_t units = nseg * nch; // < 2^31 (fft_launch)
     const int64_t grid = std::min<int64_t>(units, (int64_t)plan.cus * fft_blocks_per_cu());
+    const FftGrid gd = fft_grid(nseg, units);
     if (fft_use_w4())
         hipLaunchKernelGGL(fir_fft4_f64_kernel<kOut>, dim3((unsigned)grid), dim3(kFft4NT), fft_lds_bytes(), s, q,
-                           plan.d_pair + (size_t)part * kFftPairTable, plan.d_tw, plan.d_task, plan.B, nseg,
-                           units, plan.c8[(size_t)part]);
+                           plan.d_pair + (size_t)part * kFftPairTable, plan.d_tw, plan.d_task, plan.B, gd,
+                           plan.c8[(size_t)part]);
     else
         hipLaunchKernelGGL(fir_fft_f64_kernel<kOut>, dim3((unsigned)grid), dim3(kFftNT), fft_lds_bytes(), s, q,
-                           plan.d_pair + (size_t)part * kFftPairTable, plan.d_tw, plan.d_task, plan.B, nseg,
-                           units, plan.c8[(size_t)part]);
+                           plan.d_pair + (size_t)part * kFftPairTable, plan.d_tw, plan.d_task, plan.B, gd,
+                           plan.c8[(size_t)part]);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         err = hipGetErrorString(e);
@@ -1200,10 +1271,10 @@ inline bool fft16_launch(const FftPlan &plan, const DirectParams &q, int nch, hi
     }();
     (void)attr;
     const int64_t nseg = (q.end - q.start + plan.B - 1) / plan.B;
-    const int64_t units = nseg * nch;
+    const int64_t units = nseg * nch; // < 2^31 (fft_launch)
     const int64_t grid = std::min<int64_t>(units, (int64_t)plan.cus);
     hipLaunchKernelGGL(fir_fft16_f64_kernel<kFftOutSym>, dim3((unsigned)grid), dim3(kFft16NT), fft16_lds_bytes(), s, q,
-                       plan.d_pair16, plan.d_tw, plan.B, nseg, units);
+                       plan.d_pair16, plan.d_tw, plan.B, fft_grid(nseg, units));
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         err = hipGetErrorString(e);
@@ -1227,6 +1298,8 @@ inline size_t fft_scratch_doubles(const FftPlan &plan, const DirectParams &p, in
 // Filter outputs [p.start, p.end) of nch channels.  p.half / p.ntaps are the
 // filter's own (the plan holds the partitioning); a partitioned filter needs
 // p.y64 = fft_scratch_doubles() of scratch, owned by the caller's stream.
+inline bool fft_launch_group(const FftPlan &plan, const DirectParams &p, int nch, hipStream_t s,
+                             std::string &err);
 inline bool fft_launch(const FftPlan &plan, const DirectParams &p, int nch, hipStream_t s,
                        std::string &err) {
     if (p.end - p.start <= 0 || nch <= 0) return true;
@@ -1238,6 +1311,22 @@ inline bool fft_launch(const FftPlan &plan, const DirectParams &p, int nch, hipS
         err = "partitioned filter without partial-sum scratch";
         return false;
     }
+    // the kernels index units in 32 bits (FftGrid): channel groups keep every
+    // launch's channels x segments below 2^31 (the partial-sum scratch is
+    // reused by each group in stream order)
+    const int64_t nseg = (std::min(p.end - p.start, fft_chunk_outputs(plan)) + plan.B - 1) / plan.B;
+    const int group = (int)std::max<int64_t>(1, std::min<int64_t>(nch, (((int64_t)1 << 31) - 1) / nseg));
+    for (int c0 = 0; c0 < nch; c0 += group) {
+        DirectParams q = p;
+        q.x = p.x + (int64_t)c0 * p.x_stride;
+        q.y = p.y + (int64_t)c0 * p.y_stride;
+        if (p.peak) q.peak = p.peak + (int64_t)c0 * p.peak_stride;
+        if (!fft_launch_group(plan, q, std::min(group, nch - c0), s, err)) return false;
+    }
+    return true;
+}
+inline bool fft_launch_group(const FftPlan &plan, const DirectParams &p, int nch, hipStream_t s,
+                             std::string &err) {
     const int64_t chunk = fft_chunk_outputs(plan);
     for (int64_t cs = p.start; cs < p.end; cs += chunk) {
         DirectParams q = p;

@@ -143,16 +143,17 @@ __device__ __forceinline__ int fft16_tid() {
 // (kOut = kFftOutSym only) so that host-only builds of the header emit nothing.
 template <int kOut>
 __global__ __launch_bounds__(kFft16NT) void fir_fft16_f64_kernel(DirectParams p, const double2 *__restrict__ pair,
-                                                                const double2 *__restrict__ tw, int B, int64_t nseg,
-                                                                int64_t units) {
+                                                                const double2 *__restrict__ tw, int B,
+                                                                FftGrid gd) {
     extern __shared__ double2 flds[];
     double2 *twl = flds + kFftM; // kFftTw twiddles, LDS-resident
     for (int i = threadIdx.x; i < kFftTw; i += kFft16NT) twl[i] = tw[i];
     const int m0 = (int)((threadIdx.x & 32) << 4) + (int)(((threadIdx.x >> 6) << 5) | (threadIdx.x & 31)); // 512 h + b
     float2 v[8];
     {
-        const int64_t u = fft_unit(0, blockIdx.x, gridDim.x, units);
-        fft16_load_unit(p, (int)(u / nseg), p.start + (u % nseg) * B, m0, v);
+        const int u = fft_unit32(0, blockIdx.x, gridDim.x, gd.units);
+        const int c0 = fft_div(u, gd);
+        fft16_load_unit(p, c0, p.start + (int64_t)(u - c0 * gd.nseg) * B, m0, v);
     }
     __builtin_amdgcn_s_waitcnt(kVmcnt0);
     __syncthreads();
@@ -160,12 +161,12 @@ __global__ __launch_bounds__(kFft16NT) void fir_fft16_f64_kernel(DirectParams p,
     int pk_ch = -1;
     float *pk_lds = reinterpret_cast<float *>(twl + kFftTw);
     int pk_pending = -1;
-    int64_t rnd = 0;
-    for (int64_t u = fft_unit(0, blockIdx.x, gridDim.x, units); u < units;
-         u = fft_unit(++rnd, blockIdx.x, gridDim.x, units)) {
+    int rnd = 0;
+    for (int u = fft_unit32(0, blockIdx.x, gridDim.x, gd.units); u < gd.units;
+         u = fft_unit32(++rnd, blockIdx.x, gridDim.x, gd.units)) {
     const int par = (int)(rnd & 1);
-    const int ch = (int)(u / nseg);
-    const int64_t n0 = p.start + (u % nseg) * B;
+    const int ch = fft_div(u, gd);
+    const int64_t n0 = p.start + (int64_t)(u - ch * gd.nseg) * B;
 
     // ---- stage 1: lane pair (b, h): 8-point DFT over a' -> swap -> radix-2
     {
@@ -247,9 +248,10 @@ __global__ __launch_bounds__(kFft16NT) void fir_fft16_f64_kernel(DirectParams p,
     // pinned behind the pair step, whose operands would otherwise share the registers
     __builtin_amdgcn_sched_barrier(0);
     {
-        const int64_t un1 = fft_unit(rnd + 1, blockIdx.x, gridDim.x, units);
-        const int64_t un = un1 < units ? un1 : u;
-        fft16_load_unit(p, (int)(un / nseg), p.start + (un % nseg) * B, m0, v);
+        const int un1 = fft_unit32(rnd + 1, blockIdx.x, gridDim.x, gd.units);
+        const int un = un1 < gd.units ? un1 : u;
+        const int cn = fft_div(un, gd);
+        fft16_load_unit(p, cn, p.start + (int64_t)(un - cn * gd.nseg) * B, m0, v);
     }
     // ---- inverse stage A' (task d' = lane): radix-8 over e2 -> beta0; * W_512^(beta0 lane)
     // in the partner's block: this wave has read it, and only this wave reads it

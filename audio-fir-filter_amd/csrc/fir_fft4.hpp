@@ -170,16 +170,17 @@ template <int kOut>
 __global__ __launch_bounds__(kFft4NT) void fir_fft4_f64_kernel(DirectParams p, const double2 *__restrict__ pair,
                                                               const double2 *__restrict__ tw,
                                                               const uint32_t *__restrict__ task, int B,
-                                                              int64_t nseg, int64_t units, double2 c8) {
+                                                              FftGrid gd, double2 c8) {
     extern __shared__ double2 flds[];
     double2 *twl = flds + kFftM;
     for (int i = threadIdx.x; i < kFftTw; i += kFft4NT) twl[i] = tw[i];
     float2 v[2][16];
     {
-        const int64_t u = fft_unit(0, blockIdx.x, gridDim.x, units);
+        const int u = fft_unit32(0, blockIdx.x, gridDim.x, gd.units);
+        const int c0 = fft_div(u, gd);
 #pragma unroll
         for (int h = 0; h < 2; ++h)
-            fft_load_unit(p, (int)(u / nseg), p.start + (u % nseg) * B, threadIdx.x + kFft4NT * h, v[h]);
+            fft_load_unit(p, c0, p.start + (int64_t)(u - c0 * gd.nseg) * B, threadIdx.x + kFft4NT * h, v[h]);
     }
     __builtin_amdgcn_s_waitcnt(kVmcnt0);
     __syncthreads();
@@ -192,15 +193,15 @@ __global__ __launch_bounds__(kFft4NT) void fir_fft4_f64_kernel(DirectParams p, c
     double2 wt[2][16];
 #pragma unroll
     for (int h = 0; h < 2; ++h) powers16(twl[threadIdx.x + kFft4NT * h], wt[h]);
-    int64_t rnd = 0;
-    for (int64_t u = fft_unit(0, blockIdx.x, gridDim.x, units); u < units;
-         u = fft_unit(++rnd, blockIdx.x, gridDim.x, units)) {
+    int rnd = 0;
+    for (int u = fft_unit32(0, blockIdx.x, gridDim.x, gd.units); u < gd.units;
+         u = fft_unit32(++rnd, blockIdx.x, gridDim.x, gd.units)) {
     int jt = threadIdx.x;
     asm volatile("" : "+v"(jt));
     const int lane = jt & 63;
     const int wv = jt >> 6; // this kernel's wave (0..3); halves h = 0, 1 are 8-wave waves wv, wv + 4
-    const int ch = (int)(u / nseg);
-    const int64_t n0 = p.start + (u % nseg) * B;
+    const int ch = fft_div(u, gd);
+    const int64_t n0 = p.start + (int64_t)(u - ch * gd.nseg) * B;
 
     // ---- stage 1, both halves: thread b = jt + 256 h, 16-point DFT over z[512 a + b]
 #pragma unroll
@@ -305,11 +306,12 @@ __global__ __launch_bounds__(kFft4NT) void fir_fft4_f64_kernel(DirectParams p, c
     }
     // ---- prefetch the next unit's samples (both halves)
     {
-        const int64_t un1 = fft_unit(rnd + 1, blockIdx.x, gridDim.x, units);
-        const int64_t un = un1 < units ? un1 : u;
+        const int un1 = fft_unit32(rnd + 1, blockIdx.x, gridDim.x, gd.units);
+        const int un = un1 < gd.units ? un1 : u;
+        const int cn = fft_div(un, gd);
 #pragma unroll
         for (int h = 0; h < 2; ++h)
-            fft_load_unit(p, (int)(un / nseg), p.start + (un % nseg) * B, jt + kFft4NT * h, v[h]);
+            fft_load_unit(p, cn, p.start + (int64_t)(un - cn * gd.nseg) * B, jt + kFft4NT * h, v[h]);
     }
     wave_lds_sync();
     // ---- stage B': lane (d1, beta0) gathers e1; radix-8 -> gamma0; * W_64^(gamma0 d1)

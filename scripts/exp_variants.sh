@@ -1,5 +1,5 @@
 #!/bin/bash
-# Time alternative builds of liblcfir.so (gpurun_variants/*.so) with bench.py,
+# Time alternative builds of liblcfir.so (abvar/*.so) with bench.py,
 # parity leg on (rms vs the long-double oracle is printed per run).  Each
 # variant is copied over the package library and the original restored.
 set -u -o pipefail
@@ -8,7 +8,7 @@ cd "$ROOT"
 mkdir -p gpurun_out
 cp audio-fir-filter_amd/liblcfir.so /tmp/liblcfir_orig.so
 for rep in 1 2; do
-for so in gpurun_variants/*.so; do
+for so in abvar/*.so; do
     cp "$so" audio-fir-filter_amd/liblcfir.so
     out=$(timeout -k 10 300 python bench.py --steps 30 --warmup 3 --no-cpu-baseline "$@" 2>gpurun_out/variant_err.log | grep '^{')
     rc=$?

@@ -91,9 +91,10 @@ def test_v5_hazard_detector_is_live():
 
 
 def test_fft_unit_is_a_bijection_per_round(tmp_path):
-    """fft_unit (the persistent grid's unit order) compiled host-only from the
+    """fft_unit (the persistent grid's unit order) and fft_div compiled host-only from the
     header and run here: one-to-one per round, XCD-aware full rounds, identity
-    on the last partial round (tests/cpp/fft_unit_check.hip)."""
+    on the last partial round, the 32-bit map equal to the 64-bit one, and the
+    multiply-shift u / nseg exact for u < 2^31 (tests/cpp/fft_unit_check.hip)."""
     import shutil
     import subprocess
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
