@@ -106,7 +106,10 @@ constexpr int kNtStore = 2;
 constexpr int kFftOutF32 = 0, kFftOutFirst = 1, kFftOutAdd = 2, kFftOutLast = 3, kFftOutSym = 4;
 // kFftOutSym = kFftOutF32 for a linear-phase filter in zero-phase form: real
 // pair table (fft_plan_build's symmetric layout), outputs c in [half, L - half)
-constexpr int kFftSymSD = 0, kFftSymW = 8 * kFftNT; // double2 (2S, 2D) per (slot, thread); double2 W of slot 0
+// zero-phase table: double2 (p1, q2) per (slot, thread), then double2 (p2 of
+// slot 2m, p2 of slot 2m+1) per (m, thread) -- fft_pair_sym's coefficients,
+// computed on the host in long double (fft_plan_build)
+constexpr int kFftSymPQ = 0, kFftSymP2 = 8 * kFftNT;
 
 // Wave 0, lanes 32..63: the column-0 task pairs (d1A | e1A << 3 | d1B << 6 |
 // e1B << 9), ordered so the exchange-2 reads and exchange-3 writes stay
@@ -552,11 +555,12 @@ __device__ __forceinline__ void fft_pair(double2 P, double2 Q, double2 W, double
 }
 
 // The same pair for a linear-phase (symmetric) filter in zero-phase form
-// (kFftOutSym): G is real, so 2S = s2 and 2D = d2 are real, P1 and Q2 real and
-// P2 = i p2 imaginary -- 11 f64 operations instead of ~26.
-__device__ __forceinline__ void fft_pair_sym(double2 P, double2 Q, double2 W, double s2, double d2,
+// (kFftOutSym): G is real, so 2S = s2 and 2D = d2 are real, P1 = p1 and Q2 =
+// q2 real and P2 = i p2 imaginary, p1 = s2 + d2 Im W, q2 = s2 - d2 Im W, p2 =
+// d2 Re W.  The table holds p1, q2, p2 per bin (kFftSymPQ, kFftSymP2): 8 f64
+// operations per pair instead of ~26.
+__device__ __forceinline__ void fft_pair_sym(double2 P, double2 Q, double p1, double q2, double p2,
                                              double2 &oP, double2 &oQ) {
-    const double p1 = __builtin_fma(d2, W.y, s2), q2 = __builtin_fma(-d2, W.y, s2), p2 = d2 * W.x;
     // oP = conj(P p1 + conj(Q) i p2),  oQ = conj(Q) q2 - P i p2
     oP = make_double2(__builtin_fma(p1, P.x, p2 * Q.y), -__builtin_fma(p1, P.y, p2 * Q.x));
     oQ = make_double2(__builtin_fma(q2, Q.x, p2 * P.y), -__builtin_fma(q2, Q.y, p2 * P.x));
@@ -761,17 +765,14 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     // ---- pair-table loads, issued ahead of stage C (L2 latency off the path)
     constexpr bool kSym = kOut == kFftOutSym;
     double2 qs[kSym ? 1 : 8], qd[kSym ? 1 : 8]; // 2 S and 2 D of the pair in slot i
-    double qsr[8], qdr[8];                       // kSym: the real 2 S and 2 D
-    double2 wbase;                               // W_L^k of slot 0
+    double2 qpq[kSym ? 8 : 1], qp2[kSym ? 4 : 1]; // kSym: (p1, q2) of slot i, p2 of slots 2m, 2m+1
+    double2 wbase;                                // W_L^k of slot 0 (general form)
     if constexpr (kSym) {
-        const double2 *t = pair + kFftSymSD + j;
-        wbase = pair[kFftSymW + j];
+        const double2 *t = pair + j;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const double2 sd = t[512 * i]; // one 16-byte load per slot
-            qsr[i] = sd.x;
-            qdr[i] = sd.y;
-        }
+        for (int i = 0; i < 8; ++i) qpq[i] = t[kFftSymPQ + 512 * i]; // one 16-byte load per slot
+#pragma unroll
+        for (int m = 0; m < 4; ++m) qp2[m] = t[kFftSymP2 + 512 * m];
     } else {
         const double2 *t = pair + j;
         wbase = pair[2 * kFftPairSlots * 512 + j];
@@ -808,17 +809,17 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
         // into the generic layout first (fft_w0_permute_in).
         const bool w0 = __builtin_amdgcn_readfirstlane(w) == 0;
         const bool sp = w0 && lane == kFftSpecialLane;
-        double2 wb_hi = wbase; // W base of slots 4..7
+        double2 wb_hi = wbase; // W base of slots 4..7 (general form; the zero-phase table has per-bin p1, q2, p2)
         double2 v4 = x1[4];    // special lane: B_4, bin M/2 (slot 8, W = -i): P1 = 2S - 2D, P2 = 0
         if (w0) {
             v4 = cconj(cmul(v4, c8)); // a kernel argument (SGPRs: no L2 wait here)
-            wb_hi = csel(sp, make_double2(0.0, 1.0), wbase);
+            if constexpr (!kSym) wb_hi = csel(sp, make_double2(0.0, 1.0), wbase);
             fft_w0_permute_in(x0, x1, sp);
         }
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             if constexpr (kSym)
-                fft_pair_sym(x0[i], x1[7 - i], fft_pair_w(i < 4 ? wbase : wb_hi, i), qsr[i], qdr[i], x0[i],
+                fft_pair_sym(x0[i], x1[7 - i], qpq[i].x, qpq[i].y, (i & 1) ? qp2[i >> 1].y : qp2[i >> 1].x, x0[i],
                              x1[7 - i]);
             else
                 fft_pair(x0[i], x1[7 - i], fft_pair_w(i < 4 ? wbase : wb_hi, i), qs[i], qd[i], x0[i],
@@ -929,7 +930,11 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     if (n0 + B <= p.end) {
         // every output of this unit is before `end`: the pair (c, c+1) is
         // valid iff cmin <= c < cmax (cmin, cmax and o are even), so both
-        // stores share one offset and may merge into a dwordx2
+        // stores share one offset and may merge into a dwordx2.  (A resource
+        // over the unit's B outputs, letting the range check drop the rest,
+        // with a sign-bit mask for the peak removed the SGPR spills but
+        // measured 2 % slower: the compares this form hoists fill VALU gaps
+        // of the final DFT.)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int c = 2 * (j + 512 * r);
@@ -1129,9 +1134,11 @@ inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, hipSt
                     pt[(size_t)kFftPairSlots * kFftNT + o] = cplx(2 * dr, 2 * di);
                     pt[(size_t)2 * kFftPairSlots * kFftNT + o] = cplx(c, sn);
                 } else if (i < 8) {
-                    // symmetric layout: real 2S, 2D per (slot, thread), W of slot 0
-                    pt[(size_t)kFftSymSD + o] = cplx(2 * sr, 2 * dr);
-                    if (i == 0) pt[(size_t)kFftSymW + (size_t)t] = cplx(c, sn);
+                    // zero-phase layout: p1, q2, p2 per (slot, thread) (fft_pair_sym)
+                    const long double p1 = 2 * sr + 2 * dr * sn, q2 = 2 * sr - 2 * dr * sn, p2 = 2 * dr * c;
+                    pt[(size_t)kFftSymPQ + o] = cplx(p1, q2);
+                    double *p2t = reinterpret_cast<double *>(pt + kFftSymP2 + (size_t)(i >> 1) * kFftNT + (size_t)t);
+                    p2t[i & 1] = (double)p2;
                 }
                 if (i == 8 && sp) c8[(size_t)part] = cplx(2 * sr - 2 * dr, sym ? 0.0L : 2 * si - 2 * di);
             }

@@ -113,7 +113,7 @@ template <int kOut>
 struct Fft4Pair {
     static constexpr bool kSym = kOut == kFftOutSym;
     double2 qs[kSym ? 1 : 8], qd[kSym ? 1 : 8];
-    double qsr[kSym ? 8 : 1], qdr[kSym ? 8 : 1];
+    double2 qpq[kSym ? 8 : 1], qp2[kSym ? 4 : 1]; // zero-phase: (p1, q2) per slot, p2 of slots 2m, 2m+1
     double2 wbase;
 };
 
@@ -122,14 +122,11 @@ struct Fft4Pair {
 template <int kOut>
 __device__ __forceinline__ void fft4_pair_load(Fft4Pair<kOut> &q, const double2 *__restrict__ pair, int j) {
     if constexpr (Fft4Pair<kOut>::kSym) {
-        const double2 *t = pair + kFftSymSD + j;
-        q.wbase = pair[kFftSymW + j];
+        const double2 *t = pair + j;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const double2 sd = t[512 * i];
-            q.qsr[i] = sd.x;
-            q.qdr[i] = sd.y;
-        }
+        for (int i = 0; i < 8; ++i) q.qpq[i] = t[kFftSymPQ + 512 * i];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) q.qp2[m] = t[kFftSymP2 + 512 * m];
     } else {
         const double2 *t = pair + j;
         q.wbase = pair[2 * kFftPairSlots * 512 + j];
@@ -152,14 +149,14 @@ __device__ __forceinline__ void fft4_pair(double2 (&x0)[8], double2 (&x1)[8], co
     double2 v4 = x1[4];
     if (w0) {
         v4 = cconj(cmul(v4, c8));
-        wb_hi = csel(sp, make_double2(0.0, 1.0), q.wbase);
+        if constexpr (!Fft4Pair<kOut>::kSym) wb_hi = csel(sp, make_double2(0.0, 1.0), q.wbase);
         fft_w0_permute_in(x0, x1, sp);
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         if constexpr (Fft4Pair<kOut>::kSym)
-            fft_pair_sym(x0[i], x1[7 - i], fft_pair_w(i < 4 ? q.wbase : wb_hi, i), q.qsr[i], q.qdr[i], x0[i],
-                         x1[7 - i]);
+            fft_pair_sym(x0[i], x1[7 - i], q.qpq[i].x, q.qpq[i].y, (i & 1) ? q.qp2[i >> 1].y : q.qp2[i >> 1].x,
+                         x0[i], x1[7 - i]);
         else
             fft_pair(x0[i], x1[7 - i], fft_pair_w(i < 4 ? q.wbase : wb_hi, i), q.qs[i], q.qd[i], x0[i], x1[7 - i]);
     }
