@@ -1305,6 +1305,17 @@ inline size_t fft_scratch_doubles(const FftPlan &plan, const DirectParams &p, in
 // Filter outputs [p.start, p.end) of nch channels.  p.half / p.ntaps are the
 // filter's own (the plan holds the partitioning); a partitioned filter needs
 // p.y64 = fft_scratch_doubles() of scratch, owned by the caller's stream.
+// Largest unit count of one launch: 2^31 - 1 (FftGrid's 32-bit unit index);
+// LCFIR_FFT_MAX_UNITS lowers it (tests exercise the channel-group split with
+// small values)
+inline int64_t fft_max_units() {
+    static const int64_t v = [] {
+        const char *e = std::getenv("LCFIR_FFT_MAX_UNITS");
+        const long long m = e ? std::atoll(e) : 0;
+        return m >= 1 && m < (1LL << 31) ? (int64_t)m : (((int64_t)1 << 31) - 1);
+    }();
+    return v;
+}
 inline bool fft_launch_group(const FftPlan &plan, const DirectParams &p, int nch, hipStream_t s,
                              std::string &err);
 inline bool fft_launch(const FftPlan &plan, const DirectParams &p, int nch, hipStream_t s,
@@ -1322,7 +1333,7 @@ inline bool fft_launch(const FftPlan &plan, const DirectParams &p, int nch, hipS
     // launch's channels x segments below 2^31 (the partial-sum scratch is
     // reused by each group in stream order)
     const int64_t nseg = (std::min(p.end - p.start, fft_chunk_outputs(plan)) + plan.B - 1) / plan.B;
-    const int group = (int)std::max<int64_t>(1, std::min<int64_t>(nch, (((int64_t)1 << 31) - 1) / nseg));
+    const int group = (int)std::max<int64_t>(1, std::min<int64_t>(nch, fft_max_units() / nseg));
     for (int c0 = 0; c0 < nch; c0 += group) {
         DirectParams q = p;
         q.x = p.x + (int64_t)c0 * p.x_stride;

@@ -25,6 +25,7 @@ cd /tmp && export TMPDIR=/tmp
 step rocprof 600 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof_$TAG" -o bench -- \
     python3 "$ROOT/bench.py" --no-cpu-baseline --no-parity "$@"
 cp "$OUT/prof_$TAG/bench_kernel_stats.csv" "$OUT/kernel_stats_$TAG.csv"
+python3 "$ROOT/scripts/trace_exclusive.py" "$OUT/prof_$TAG/bench_kernel_trace.csv" > "$OUT/exclusive_from_trace_$TAG.json"
 i=0
 for c in FETCH_SIZE WRITE_SIZE "SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64"; do
     i=$((i+1))

@@ -395,6 +395,59 @@ def test_fft_partitioned_chunk_seams(oracle_mod, tmp_path):
     assert pk == np.abs(y).max()
 
 
+_GROUP_CHILD = """
+import sys, numpy as np
+sys.path[:0] = [{pkg!r}, {oracle!r}]
+import lcfir, synth
+nch, n = 5, {n}
+x = synth.file_buffer(nch, n, 48000.0, file=8, bits=24)
+out = {{}}
+for name in ("sym", "part"):
+    flt = lcfir.Filter(np.load({taps!r}.replace("NAME", name)), method="fft")
+    dx = lcfir.DeviceBuffer.from_array(x); dy = lcfir.DeviceBuffer(x.nbytes)
+    pk = lcfir.DeviceBuffer.from_array(np.zeros(nch, np.float32))
+    flt.filter_channels_dev(dx, n, nch, n, dy, n, pk)
+    lcfir.sync()
+    out["y_" + name] = dy.download((nch, n))
+    out["pk_" + name] = pk.download((nch,), np.float32)
+np.savez({out!r}, **out)
+"""
+
+
+@pytest.mark.parametrize("max_units", [7, 20])
+def test_fft_channel_groups(tmp_path, max_units):
+    """The kernels index units in 32 bits, so fft_launch splits a launch into
+    channel groups of at most 2^31 - 1 units (fir_fft.hpp FftGrid).
+    LCFIR_FFT_MAX_UNITS (read once per process: child processes) forces the
+    split at small sizes -- one channel per launch (7) and groups of two (20,
+    9 segments per channel) -- for a zero-phase and a partitioned filter, with
+    per-channel peaks: every output and peak bit-identical to one launch."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    import lcfir
+    np.save(tmp_path / "sym.npy", lcfir.design_lowcut(20.0, 4.0, 48000.0))
+    np.save(tmp_path / "part.npy", lcfir.design_lowcut(20.0, 10.0, 48000.0))
+    res = {}
+    for mu in (None, max_units):
+        out = tmp_path / f"y_{mu}.npz"
+        code = _GROUP_CHILD.format(pkg=os.path.join(root, "audio-fir-filter_amd"),
+                                   oracle=os.path.join(root, "oracle"), n=100_000,
+                                   taps=str(tmp_path / "NAME.npy"), out=str(out))
+        env = dict(os.environ)
+        env.pop("LCFIR_FFT_MAX_UNITS", None)
+        if mu:
+            env["LCFIR_FFT_MAX_UNITS"] = str(mu)
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                           timeout=600)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res[mu] = np.load(out)
+    for k in res[None].files:
+        assert np.array_equal(res[None][k], res[max_units][k]), k
+    assert np.all(res[None]["pk_sym"] > 0)
+
+
 # ---- linear-phase filters: the zero-phase form (fir_fft.hpp fft_sym_eligible)
 _SYM_CHILD = """
 import sys, numpy as np
