@@ -105,6 +105,13 @@ class Backend:
         self.normalize(yw, nch, count, peaks, slot, force)
         self.zero_peaks(clear)
 
+    def filter_normalize_prev(self, xw, x_lo, x_hi, n, nch, yw, start, end, peaks, slot: int,
+                              prev_yw, prev_count: int, prev_slot: int, force: bool):
+        """filter, plus the previous shard's per-file normalize (slot prev_slot,
+        final already).  A device backend fuses the two into one launch."""
+        self.filter(xw, x_lo, x_hi, n, nch, yw, start, end, peaks, slot)
+        self.normalize(prev_yw, nch, prev_count, peaks, prev_slot, force)
+
     def new_peaks(self, nfiles: int):
         raise NotImplementedError
 
@@ -136,7 +143,8 @@ class BatchRunner:
 
     def __init__(self, backend: Backend, rank: int, world: int, nframes: Sequence[int], nch: int,
                  half: int, normalize: bool = False, peak_scope: str = "file",
-                 allreduce_max: Optional[Callable] = None, lanes: int = 1):
+                 allreduce_max: Optional[Callable] = None, lanes: int = 1,
+                 fuse_normalize: bool = True):
         if peak_scope not in ("file", "global"):
             raise ValueError("peak_scope must be 'file' or 'global'")
         if lanes < 1:
@@ -158,6 +166,11 @@ class BatchRunner:
         if self.exchange and allreduce_max is None:
             raise ValueError("this plan needs a MAX all-reduce of the peak vector")
         self.allreduce_max = allreduce_max
+        # Without an exchange, a file's peak is final when its own filter is
+        # done: its normalize then rides in the NEXT shard's filter launch
+        # (Backend.filter_normalize_prev) and only the last shard's runs as a
+        # pass of its own.  With an exchange every normalize waits for it.
+        self.fuse = fuse_normalize and not self.exchange and peak_scope == "file"
         # per lane, two peak vectors alternating by step: a step's last
         # normalize launch also zeroes the other one for the lane's next step,
         # so no separate reset launch sits in the step
@@ -205,13 +218,23 @@ class BatchRunner:
         outputs = self._outs[lane]
         peaks = self._peak_bufs[lane][self._cur[lane]]      # zero (prepare, or the lane's previous step)
         nxt = self._peak_bufs[lane][1 - self._cur[lane]]
+        prev = None
         for sh, (xw, lo, hi), yw in zip(self.shards, self.inputs, outputs):
-            self.b.filter(xw, lo, hi, self.nframes[sh.file], self.nch, yw, sh.start, sh.end,
-                          peaks, sh.file)
+            if self.fuse and prev is not None:
+                psh, pyw = prev
+                self.b.filter_normalize_prev(xw, lo, hi, self.nframes[sh.file], self.nch, yw, sh.start,
+                                             sh.end, peaks, sh.file, pyw, psh.end - psh.start, psh.file,
+                                             self.normalize)
+            else:
+                self.b.filter(xw, lo, hi, self.nframes[sh.file], self.nch, yw, sh.start, sh.end,
+                              peaks, sh.file)
+            prev = (sh, yw)
         if self.exchange:
             self.allreduce_max(peaks)
         last = len(self.shards) - 1
         for i, (sh, yw) in enumerate(zip(self.shards, outputs)):
+            if self.fuse and i < last:
+                continue  # rescaled inside the next shard's filter launch
             slot = None if self.scope == "global" else sh.file
             if i == last:
                 self.b.normalize_clear(yw, self.nch, sh.end - sh.start, peaks, slot, self.normalize,
@@ -300,6 +323,16 @@ class DeviceBackend(Backend):
     def normalize(self, yw, nch, count, peaks, slot, force):
         p = peaks if slot is None else peaks[slot:slot + 1]
         self.lc.normalize_dev(yw, yw.shape[1], nch, count, p, p.numel(), force, self.sp)
+
+    def filter_normalize_prev(self, xw, x_lo, x_hi, n, nch, yw, start, end, peaks, slot,
+                              prev_yw, prev_count, prev_slot, force):
+        if not prev_yw.is_contiguous() or prev_yw.shape[1] != prev_count:
+            return super().filter_normalize_prev(xw, x_lo, x_hi, n, nch, yw, start, end, peaks, slot,
+                                                 prev_yw, prev_count, prev_slot, force)
+        self.flt.filter_window_norm_dev(xw, x_lo, x_hi, xw.shape[1], n, nch, yw, start, yw.shape[1],
+                                        start, end, peaks[slot:slot + 1], 0, prev_yw,
+                                        prev_yw.numel(), peaks[prev_slot:prev_slot + 1], 1, force,
+                                        self.sp)
 
     def normalize_clear(self, yw, nch, count, peaks, slot, force, clear):
         p = peaks if slot is None else peaks[slot:slot + 1]

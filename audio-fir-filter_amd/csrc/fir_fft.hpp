@@ -625,6 +625,68 @@ __device__ __forceinline__ void fft_peak_commit(const DirectParams &p, int ch, c
     atomicMax(p.peak + ch * p.peak_stride, __float_as_uint(pk));
 }
 
+// A previous file's normalize (ProcessFile.cp:98-101), carried by this
+// launch: its outputs y[0, count) (contiguous, 16-B aligned) are rescaled by
+// 1/peak iff max(peak[0, npeak)) > 1 or force -- normalize_kernel's rule and
+// arithmetic, (float)((double)v * (1.0 / peak)), so bit-identical.  Unit u
+// takes y[u slice, (u + 1) slice); the older waves of the workgroup (0..3)
+// do it while they wait at the segment's second barrier for the younger
+// ones (DESIGN.md s8 timeline), so a batch step needs one normalize pass
+// (its last file's) instead of one per file.
+struct FftNrm {
+    float *y = nullptr;
+    const unsigned *peak = nullptr;
+    int64_t count = 0;
+    int64_t slice = 0; // floats per unit, a multiple of 1024 (fft_launch)
+    int32_t npeak = 0;
+    int32_t force = 0;
+};
+// The older waves load, rescale and store their unit's slice while they wait
+// at the segment's second barrier; the stores' completion is waited for only
+// at the next unit's output stores.  Branch-free: a buffer resource over
+// exactly the slice drops the lanes past its end (a divergent guard made the
+// compiler wait for every earlier load before each one).  kNrmK 16-byte
+// loads per thread, all in flight: slices of up to 14 336 floats
+// (fft_nrm_fusable).  Non-temporal: the 8 B/sample stream must not evict the
+// pair table and the halo samples the filter re-reads from L2.  (Deferring
+// the rescale to the next barrier 1 kept kNrmK float4 live across the final
+// phase: 256 VGPRs and scratch spills.)
+constexpr int kNrmK = 14;
+constexpr int kVmcntNrm = 0x0F70 | kNrmK; // s_waitcnt vmcnt(kNrmK): the slice's stores may stay in flight
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t fft_nrm_rsrc(const FftNrm &nrm, int u, bool active = true) {
+    const int64_t s0 = (int64_t)u * nrm.slice;
+    const int64_t s1 = s0 + nrm.slice < nrm.count ? s0 + nrm.slice : nrm.count;
+    const int len = active && s1 > s0 ? (int)(s1 - s0) : 0;
+    return __builtin_amdgcn_make_buffer_rsrc(nrm.y + (s0 < nrm.count ? s0 : 0), (short)0, 4 * (len & ~3), 0x00020000);
+}
+// unconditional for every wave (an inactive one loads through an empty
+// resource: no memory traffic), so v is defined on every path and never
+// live across the column phase
+__device__ __forceinline__ void fft_nrm_load(const FftNrm &nrm, int u, int t, bool active, float4 (&v)[kNrmK]) {
+    const __amdgpu_buffer_rsrc_t r = fft_nrm_rsrc(nrm, u, active);
+#pragma unroll
+    for (int k = 0; k < kNrmK; ++k)
+        v[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, 16 * t + 4096 * k, 0, kNtStore));
+}
+__device__ __forceinline__ void fft_nrm_store(const FftNrm &nrm, int u, int t, double gain, float4 (&v)[kNrmK]) {
+    const __amdgpu_buffer_rsrc_t r = fft_nrm_rsrc(nrm, u);
+    using b128_t = decltype(__builtin_amdgcn_raw_buffer_load_b128(r, 0, 0, 0));
+#pragma unroll
+    for (int k = 0; k < kNrmK; ++k) {
+        v[k].x = (float)((double)v[k].x * gain);
+        v[k].y = (float)((double)v[k].y * gain);
+        v[k].z = (float)((double)v[k].z * gain);
+        v[k].w = (float)((double)v[k].w * gain);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(b128_t, v[k]), r, 16 * t + 4096 * k, 0, kNtStore);
+    }
+    // the last 1..3 floats when count is not a multiple of 4
+    const int64_t s0 = (int64_t)u * nrm.slice;
+    const int64_t s1 = s0 + nrm.slice < nrm.count ? s0 + nrm.slice : nrm.count;
+    const int64_t tail = nrm.count & ~(int64_t)3;
+    if (s1 == nrm.count && tail >= s0 && tail + t < nrm.count)
+        nrm.y[tail + t] = (float)((double)nrm.y[tail + t] * gain);
+}
+
 // Persistent: one workgroup per CU walks the units u = blockIdx.x + i * gridDim.x
 // of the nch x nseg (channel, segment) grid.  The next unit's samples are
 // loaded during the current unit's final phase, so HBM latency is off the path.
@@ -642,13 +704,24 @@ __device__ __forceinline__ void fft_peak_commit(const DirectParams &p, int ch, c
 //   kFftOutAdd   : add it to p.y64;
 //   kFftOutLast  : RNE(p.y64 + partial) to f32 into y, fused peak.
 // c8 = the special lane's bin-M/2 coefficient 2S - 2D of this pair table.
-template <int kOut>
+// kNrm: the launch also rescales a previous file's outputs (FftNrm).
+template <int kOut, bool kNrm = false>
 __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, const double2 *__restrict__ pair,
                                                             const double2 *__restrict__ tw,
                                                             const uint32_t *__restrict__ task, int B,
-                                                            FftGrid gd, double2 c8) {
+                                                            FftGrid gd, double2 c8, FftNrm nrm) {
     extern __shared__ double2 flds[];
     FFT_USTAMP(0);
+    // kNrm: the normalize decision, once per launch (uniform)
+    bool nrm_on = false;
+    double nrm_gain = 1.0;
+    if constexpr (kNrm) {
+        float pkv = 0.0f;
+        for (int i = 0; i < nrm.npeak; ++i) pkv = fmaxf(pkv, __uint_as_float(nrm.peak[i]));
+        nrm_on = (pkv > 1.0f || nrm.force) && pkv > 0.0f;
+        nrm_gain = 1.0 / (double)pkv;
+    }
+
     double2 *twl = flds + kFftM; // the kFftTw twiddles, LDS-resident
     for (int i = threadIdx.x; i < kFftTw; i += kFftNT) twl[i] = tw[i];
     float2 v[16]; // samples of the unit about to start
@@ -900,7 +973,24 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
 #pragma unroll
     for (int g1 = 0; g1 < 8; ++g1) blk1[lane + 64 * g1] = x1[g1];
     FFT_STAMP(11);
-    __syncthreads();
+    if constexpr (kNrm) {
+        // waves 0..3 reach this barrier well before waves 4..7: they spend
+        // the wait on this unit's slice of the previous file's normalize
+        // (loads, rescale and stores here; the stores' completion is waited
+        // for only at the next unit's output stores, kVmcntNrm)
+        if (nrm_on && w < 4) {
+            float4 nv[kNrmK];
+            fft_nrm_load(nrm, u, j, true, nv);
+            fft_nrm_store(nrm, u, j, nrm_gain, nv);
+        }
+        // an LDS-only barrier: __syncthreads() would first wait for those
+        // global stores to complete (its release fence covers every space)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    } else {
+        __syncthreads();
+    }
     FFT_STAMP(12);
 
     // ---- final: thread b = j gathers its 16 columns, * W_8192^(b c), 16-point DFT -> v[512 a + b]
@@ -915,7 +1005,12 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     // trick), m = 512 r + j, valid for c >= T-1.  Range-checked buffer over
     // y[start, end): invalid lanes store to an out-of-range offset, which the
     // hardware drops (no branches).
-    __builtin_amdgcn_s_waitcnt(kVmcnt0); // the prefetch has landed long ago (see the loop head)
+    // the prefetch has landed long ago (see the loop head); kNrm: the older
+    // waves leave their normalize slice's stores (the newest kNrmK) in flight
+    if (kNrm && nrm_on && w < 4)
+        __builtin_amdgcn_s_waitcnt(kVmcntNrm);
+    else
+        __builtin_amdgcn_s_waitcnt(kVmcnt0);
     float *yb = p.y + (int64_t)ch * p.y_stride + (p.start - p.y_lo);
     const __amdgpu_buffer_rsrc_t ys = __builtin_amdgcn_make_buffer_rsrc(
         yb, (short)0, (int)((p.end - p.start) * 4), 0x00020000);
@@ -1239,11 +1334,11 @@ inline int64_t fft_chunk() {
     return v;
 }
 
-template <int kOut>
+template <int kOut, bool kNrm = false>
 inline bool fft_launch_one(const FftPlan &plan, const DirectParams &q, int part, int nch, hipStream_t s,
-                           std::string &err) {
+                           std::string &err, FftNrm nrm = FftNrm{}) {
     static const bool attr = [] {
-        return hipFuncSetAttribute(reinterpret_cast<const void *>(&fir_fft_f64_kernel<kOut>),
+        return hipFuncSetAttribute(reinterpret_cast<const void *>(&fir_fft_f64_kernel<kOut, kNrm>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)fft_lds_bytes()) == hipSuccess &&
                hipFuncSetAttribute(reinterpret_cast<const void *>(&fir_fft4_f64_kernel<kOut>),
@@ -1255,14 +1350,26 @@ inline bool fft_launch_one(const FftPlan &plan, const DirectParams &q, int part,
     const int64_t units = nseg * nch; // < 2^31 (fft_launch)
     const int64_t grid = std::min<int64_t>(units, (int64_t)plan.cus * fft_blocks_per_cu());
     const FftGrid gd = fft_grid(nseg, units);
-    if (fft_use_w4())
+    if constexpr (kNrm) {
+        // the previous file's floats over this launch's units, whole 1 024-float
+        // blocks, at most kNrmK per thread (fft_nrm_fits)
+        const int64_t per = (nrm.count + units - 1) / units;
+        nrm.slice = (per + 1023) / 1024 * 1024;
+        if (nrm.slice > (int64_t)kNrmK * 1024) {
+            err = "normalize slice too large to fuse";
+            return false;
+        }
+        hipLaunchKernelGGL((fir_fft_f64_kernel<kOut, true>), dim3((unsigned)grid), dim3(kFftNT), fft_lds_bytes(),
+                           s, q, plan.d_pair + (size_t)part * kFftPairTable, plan.d_tw, plan.d_task, plan.B, gd,
+                           plan.c8[(size_t)part], nrm);
+    } else if (fft_use_w4())
         hipLaunchKernelGGL(fir_fft4_f64_kernel<kOut>, dim3((unsigned)grid), dim3(kFft4NT), fft_lds_bytes(), s, q,
                            plan.d_pair + (size_t)part * kFftPairTable, plan.d_tw, plan.d_task, plan.B, gd,
                            plan.c8[(size_t)part]);
     else
-        hipLaunchKernelGGL(fir_fft_f64_kernel<kOut>, dim3((unsigned)grid), dim3(kFftNT), fft_lds_bytes(), s, q,
-                           plan.d_pair + (size_t)part * kFftPairTable, plan.d_tw, plan.d_task, plan.B, gd,
-                           plan.c8[(size_t)part]);
+        hipLaunchKernelGGL((fir_fft_f64_kernel<kOut, false>), dim3((unsigned)grid), dim3(kFftNT), fft_lds_bytes(),
+                           s, q, plan.d_pair + (size_t)part * kFftPairTable, plan.d_tw, plan.d_task, plan.B, gd,
+                           plan.c8[(size_t)part], FftNrm{});
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         err = hipGetErrorString(e);
@@ -1317,9 +1424,25 @@ inline int64_t fft_max_units() {
     return v;
 }
 inline bool fft_launch_group(const FftPlan &plan, const DirectParams &p, int nch, hipStream_t s,
-                             std::string &err);
+                             std::string &err, const FftNrm *nrm);
+// Can fft_launch carry a previous file's normalize (FftNrm) in its first
+// launch?  Single-partition filters on the default kernel, 16-B aligned
+// buffer; otherwise the caller runs the normalize pass itself.
+// The first launch (the one that carries it) must spread the previous
+// file's floats at <= kNrmK x 1 024 per unit.
+inline bool fft_nrm_fusable(const FftPlan &plan, const FftNrm &nrm, const DirectParams &p, int nch) {
+    if (plan.parts != 1 || plan.waves16 || fft_use_w4() || !nrm.y || !nrm.peak || nrm.npeak < 1 ||
+        (reinterpret_cast<uintptr_t>(nrm.y) & 15) != 0 || p.end <= p.start || nch <= 0)
+        return false;
+    const int64_t nseg = (std::min(p.end - p.start, fft_chunk_outputs(plan)) + plan.B - 1) / plan.B;
+    const int64_t group = std::max<int64_t>(1, std::min<int64_t>(nch, fft_max_units() / nseg));
+    const int64_t units = nseg * group;
+    const int64_t per = (nrm.count + units - 1) / units;
+    return (per + 1023) / 1024 <= kNrmK;
+}
+// nrm: a previous file's normalize to fuse (fft_nrm_fusable must hold), or null
 inline bool fft_launch(const FftPlan &plan, const DirectParams &p, int nch, hipStream_t s,
-                       std::string &err) {
+                       std::string &err, const FftNrm *nrm = nullptr) {
     if (p.end - p.start <= 0 || nch <= 0) return true;
     if (nch > 65535) {
         err = "too many channels for one launch";
@@ -1339,12 +1462,12 @@ inline bool fft_launch(const FftPlan &plan, const DirectParams &p, int nch, hipS
         q.x = p.x + (int64_t)c0 * p.x_stride;
         q.y = p.y + (int64_t)c0 * p.y_stride;
         if (p.peak) q.peak = p.peak + (int64_t)c0 * p.peak_stride;
-        if (!fft_launch_group(plan, q, std::min(group, nch - c0), s, err)) return false;
+        if (!fft_launch_group(plan, q, std::min(group, nch - c0), s, err, c0 == 0 ? nrm : nullptr)) return false;
     }
     return true;
 }
 inline bool fft_launch_group(const FftPlan &plan, const DirectParams &p, int nch, hipStream_t s,
-                             std::string &err) {
+                             std::string &err, const FftNrm *nrm) {
     const int64_t chunk = fft_chunk_outputs(plan);
     for (int64_t cs = p.start; cs < p.end; cs += chunk) {
         DirectParams q = p;
@@ -1362,9 +1485,16 @@ inline bool fft_launch_group(const FftPlan &plan, const DirectParams &p, int nch
                 if (!fft16_launch(plan, q, nch, s, err)) return false;
                 continue;
             }
-            if (plan.sym ? !fft_launch_one<kFftOutSym>(plan, q, 0, nch, s, err)
-                         : !fft_launch_one<kFftOutF32>(plan, q, 0, nch, s, err))
-                return false;
+            // the first chunk's launch carries the fused normalize
+            const bool fuse = nrm && cs == p.start;
+            bool ok;
+            if (plan.sym)
+                ok = fuse ? fft_launch_one<kFftOutSym, true>(plan, q, 0, nch, s, err, *nrm)
+                          : fft_launch_one<kFftOutSym>(plan, q, 0, nch, s, err);
+            else
+                ok = fuse ? fft_launch_one<kFftOutF32, true>(plan, q, 0, nch, s, err, *nrm)
+                          : fft_launch_one<kFftOutF32>(plan, q, 0, nch, s, err);
+            if (!ok) return false;
             continue;
         }
         // the caller's scratch (p.y64, fft_scratch_doubles): f64 partial sums of

@@ -158,9 +158,14 @@ double *stream_scratch(lcfir_ctx *ctx, hipStream_t s, size_t need) {
     return slot->p;
 }
 
+int launch_normalize(float *d_y, int64_t stride, int32_t nch, int64_t n, const unsigned *d_peak, int32_t npeak,
+                     int force, unsigned *d_clear, int32_t nclear, hipStream_t s);
+
 // Run the filter for outputs [start, end) of nch channels.  x/y geometry as
-// in DirectParams.
-int run_filter(lcfir_ctx *ctx, lcfir::DirectParams p, int nch, hipStream_t s) {
+// in DirectParams.  nrm (nullable): a previous file's normalize, fused into
+// the FFT launch where fft_nrm_fusable, else run as its own pass afterwards.
+int run_filter(lcfir_ctx *ctx, lcfir::DirectParams p, int nch, hipStream_t s,
+               const lcfir::FftNrm *nrm = nullptr) {
     p.taps = ctx->d_taps;
     p.ntaps = ctx->ntaps;
     p.half = ctx->half;
@@ -175,11 +180,15 @@ int run_filter(lcfir_ctx *ctx, lcfir::DirectParams p, int nch, hipStream_t s) {
             p.y64 = stream_scratch(ctx, s, need);
             if (!p.y64) return fail(LCFIR_ENOMEM, "partial-sum scratch of %zu doubles", need);
         }
-        if (!lcfir::fft_launch(ctx->fft, p, nch, s, err))
+        const bool fuse = nrm && lcfir::fft_nrm_fusable(ctx->fft, *nrm, p, nch);
+        if (!lcfir::fft_launch(ctx->fft, p, nch, s, err, fuse ? nrm : nullptr))
             return fail(LCFIR_EDEVICE, "fft launch: %s", err.c_str());
-        return LCFIR_OK;
+        if (!nrm || fuse) return LCFIR_OK;
+    } else {
+        const int rc = launch_direct(p, nch, s);
+        if (rc || !nrm) return rc;
     }
-    return launch_direct(p, nch, s);
+    return launch_normalize(nrm->y, nrm->count, 1, nrm->count, nrm->peak, nrm->npeak, nrm->force, nullptr, 0, s);
 }
 
 bool ranges_overlap(const void *a, size_t an, const void *b, size_t bn) {
@@ -271,6 +280,17 @@ inline unsigned *peak_bits(float *p) { return reinterpret_cast<unsigned *>(p); }
 int stream_blocks(int64_t n, int per_block_elems) {
     int64_t b = (n + per_block_elems - 1) / per_block_elems;
     return (int)std::max<int64_t>(1, std::min<int64_t>(b, 2048));
+}
+
+int launch_normalize(float *d_y, int64_t stride, int32_t nch, int64_t n, const unsigned *d_peak, int32_t npeak,
+                     int force, unsigned *d_clear, int32_t nclear, hipStream_t s) {
+    // grid-stride: 256 blocks per channel already saturate HBM when the pass
+    // rescales, and keep the (common) no-op launch short
+    const int blocks = std::min(stream_blocks(n, 256 * 16), 256);
+    hipLaunchKernelGGL(lcfir::normalize_kernel, dim3(blocks, nch), dim3(256), 0, s, d_y, stride, n, d_peak, npeak,
+                       force, d_clear, nclear);
+    LCFIR_HIP(hipGetLastError());
+    return LCFIR_OK;
 }
 
 } // namespace
@@ -512,10 +532,10 @@ int lcfir_filter_channels_dev(lcfir_ctx *ctx, const float *d_x, int64_t x_stride
     return run_filter(ctx, p, nch, reinterpret_cast<hipStream_t>(stream));
 }
 
-int lcfir_filter_window_dev(lcfir_ctx *ctx, const float *d_xw, int64_t x_lo, int64_t x_hi,
-                            int64_t x_stride, int64_t n, int32_t nch, float *d_yw, int64_t y_lo,
-                            int64_t y_stride, int64_t start, int64_t end, float *d_peak,
-                            int64_t peak_stride, void *stream) {
+static int filter_window(lcfir_ctx *ctx, const float *d_xw, int64_t x_lo, int64_t x_hi, int64_t x_stride,
+                         int64_t n, int32_t nch, float *d_yw, int64_t y_lo, int64_t y_stride, int64_t start,
+                         int64_t end, float *d_peak, int64_t peak_stride, void *stream,
+                         const lcfir::FftNrm *nrm) {
     if (!ctx || !d_xw || !d_yw) return fail(LCFIR_EINVAL, "null argument");
     if (nch < 0 || n < 0 || start < 0 || end < start || end > n)
         return fail(LCFIR_EINVAL, "bad range [%lld, %lld) for n=%lld", (long long)start,
@@ -547,7 +567,48 @@ int lcfir_filter_window_dev(lcfir_ctx *ctx, const float *d_xw, int64_t x_lo, int
     p.end = end;
     p.peak = d_peak ? peak_bits(d_peak) : nullptr;
     p.peak_stride = peak_stride;
-    return run_filter(ctx, p, nch, reinterpret_cast<hipStream_t>(stream));
+    return run_filter(ctx, p, nch, reinterpret_cast<hipStream_t>(stream), nrm);
+}
+
+int lcfir_filter_window_dev(lcfir_ctx *ctx, const float *d_xw, int64_t x_lo, int64_t x_hi,
+                            int64_t x_stride, int64_t n, int32_t nch, float *d_yw, int64_t y_lo,
+                            int64_t y_stride, int64_t start, int64_t end, float *d_peak,
+                            int64_t peak_stride, void *stream) {
+    return filter_window(ctx, d_xw, x_lo, x_hi, x_stride, n, nch, d_yw, y_lo, y_stride, start, end, d_peak,
+                         peak_stride, stream, nullptr);
+}
+
+int lcfir_filter_window_norm_dev(lcfir_ctx *ctx, const float *d_xw, int64_t x_lo, int64_t x_hi,
+                                 int64_t x_stride, int64_t n, int32_t nch, float *d_yw, int64_t y_lo,
+                                 int64_t y_stride, int64_t start, int64_t end, float *d_peak,
+                                 int64_t peak_stride, float *d_ny, int64_t ncount, const float *d_npeak,
+                                 int32_t nnpeak, int nforce, void *stream) {
+    if (!d_ny || !d_npeak || ncount < 0 || nnpeak < 1) return fail(LCFIR_EINVAL, "bad normalize argument");
+    if (ncount == 0)
+        return lcfir_filter_window_dev(ctx, d_xw, x_lo, x_hi, x_stride, n, nch, d_yw, y_lo, y_stride, start, end,
+                                       d_peak, peak_stride, stream);
+    if (!ctx || !d_xw || !d_yw) return fail(LCFIR_EINVAL, "null argument");
+    if (nch > 0 && end > start) {
+        const size_t xb = sizeof(float) * (size_t)(x_stride * (nch - 1) + (x_hi - x_lo));
+        const size_t yb = sizeof(float) * (size_t)(y_stride * (nch - 1) + (end - y_lo));
+        const size_t nb = sizeof(float) * (size_t)ncount;
+        if (ranges_overlap(d_ny, nb, d_xw, xb) || ranges_overlap(d_ny, nb, d_yw, yb))
+            return fail(LCFIR_EINVAL, "d_ny overlaps the window or the outputs");
+    }
+    lcfir::FftNrm nrm;
+    nrm.y = d_ny;
+    nrm.peak = reinterpret_cast<const unsigned *>(d_npeak);
+    nrm.count = ncount;
+    nrm.npeak = nnpeak;
+    nrm.force = nforce ? 1 : 0;
+    if (nch == 0 || end == start) {
+        DeviceGuard g(ctx->device);
+        if (!g.ok) return fail(LCFIR_EDEVICE, "hipSetDevice(%d) failed", ctx->device);
+        return launch_normalize(d_ny, ncount, 1, ncount, nrm.peak, nnpeak, nrm.force, nullptr, 0,
+                                reinterpret_cast<hipStream_t>(stream));
+    }
+    return filter_window(ctx, d_xw, x_lo, x_hi, x_stride, n, nch, d_yw, y_lo, y_stride, start, end, d_peak,
+                         peak_stride, stream, &nrm);
 }
 
 int lcfir_peak_reset_dev(float *d_peak, int32_t count, void *stream) {
@@ -581,15 +642,9 @@ int lcfir_normalize_clear_dev(float *d_y, int64_t stride, int32_t nch, int64_t n
     if (nclear > 0 && d_clear < d_peak + npeak && d_peak < d_clear + nclear)
         return fail(LCFIR_EINVAL, "the slots to clear overlap the peak slots read");
     if (nch == 0 || n == 0) return nclear > 0 ? lcfir_peak_reset_dev(d_clear, nclear, stream) : LCFIR_OK;
-    // grid-stride: 256 blocks per channel already saturate HBM when the pass
-    // rescales, and keep the (common) no-op launch short
-    const int blocks = std::min(stream_blocks(n, 256 * 16), 256);
-    hipLaunchKernelGGL(lcfir::normalize_kernel, dim3(blocks, nch), dim3(256), 0,
-                       reinterpret_cast<hipStream_t>(stream), d_y, stride, n,
-                       reinterpret_cast<const unsigned *>(d_peak), npeak, force,
-                       nclear > 0 ? peak_bits(d_clear) : nullptr, nclear);
-    LCFIR_HIP(hipGetLastError());
-    return LCFIR_OK;
+    return launch_normalize(d_y, stride, nch, n, reinterpret_cast<const unsigned *>(d_peak), npeak, force,
+                            nclear > 0 ? peak_bits(d_clear) : nullptr, nclear,
+                            reinterpret_cast<hipStream_t>(stream));
 }
 
 int lcfir_normalize_dev(float *d_y, int64_t stride, int32_t nch, int64_t n, const float *d_peak,

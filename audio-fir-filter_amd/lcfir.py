@@ -64,6 +64,9 @@ _SIGNATURES = {
     "lcfir_filter_window_dev": (
         [_ctxp, _vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_i32, _vp, _c_i64, _c_i64, _c_i64, _c_i64,
          _vp, _c_i64, _vp], _c_int),
+    "lcfir_filter_window_norm_dev": (
+        [_ctxp, _vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_i32, _vp, _c_i64, _c_i64, _c_i64, _c_i64,
+         _vp, _c_i64, _vp, _c_i64, _vp, _c_i32, _c_int, _vp], _c_int),
     "lcfir_peak_reset_dev": ([_vp, _c_i32, _vp], _c_int),
     "lcfir_peak_dev": ([_vp, _c_i64, _c_i32, _c_i64, _vp, _vp], _c_int),
     "lcfir_normalize_dev": ([_vp, _c_i64, _c_i32, _c_i64, _vp, _c_i32, _c_int, _vp], _c_int),
@@ -255,7 +258,21 @@ def _filter_window_dev(self, d_xw, x_lo: int, x_hi: int, x_stride: int, n: int, 
         start, end, _ptr(d_peak) if d_peak is not None else None, peak_stride, stream or None))
 
 
+def _filter_window_norm_dev(self, d_xw, x_lo: int, x_hi: int, x_stride: int, n: int, nch: int,
+                            d_yw, y_lo: int, y_stride: int, start: int, end: int, d_peak,
+                            peak_stride: int, d_ny, ncount: int, d_npeak, nnpeak: int, force: bool,
+                            stream=0):
+    """lcfir_filter_window_norm_dev: filter_window_dev plus a previous file's
+    normalize of the ncount contiguous floats at d_ny (fused into the FFT
+    launch where possible; bit-identical to normalize_dev either way)."""
+    _check(load().lcfir_filter_window_norm_dev(
+        self._ctx, _ptr(d_xw), x_lo, x_hi, x_stride, n, nch, _ptr(d_yw), y_lo, y_stride,
+        start, end, _ptr(d_peak) if d_peak is not None else None, peak_stride, _ptr(d_ny), ncount,
+        _ptr(d_npeak), nnpeak, 1 if force else 0, stream or None))
+
+
 Filter.filter_window_dev = _filter_window_dev
+Filter.filter_window_norm_dev = _filter_window_norm_dev
 
 
 class ThreadSafeProgress:

@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--bits", type=int, default=24, help="0 = float32 source")
     ap.add_argument("--normalize", action="store_true")
     ap.add_argument("--peak-scope", default="file", choices=["file", "global"])
+    ap.add_argument("--no-fuse-normalize", action="store_true",
+                    help="run every file's normalize as its own pass (A/B of BatchRunner's fused form)")
     ap.add_argument("--lanes", type=int, default=None,
                     help="pipeline consecutive steps over this many streams (BatchRunner lanes): "
                          "a step's first segments fill the CUs the previous step's last round "
@@ -184,15 +186,22 @@ class TimedBackend:
     def __getattr__(self, name):
         return getattr(self.inner, name)
 
-    def filter(self, *a, **k):
+    def _timed(self, fn, *a, **k):
         if not self.record:
-            return self.inner.filter(*a, **k)
+            return fn(*a, **k)
         e0 = self.torch.cuda.Event(enable_timing=True)
         e1 = self.torch.cuda.Event(enable_timing=True)
         e0.record(self.inner.stream)
-        self.inner.filter(*a, **k)
+        fn(*a, **k)
         e1.record(self.inner.stream)
         self.events.append((e0, e1))
+
+    def filter(self, *a, **k):
+        return self._timed(self.inner.filter, *a, **k)
+
+    def filter_normalize_prev(self, *a, **k):
+        # a filter launch that also rescales the previous file (config 5)
+        return self._timed(self.inner.filter_normalize_prev, *a, **k)
 
 
 def main():
@@ -237,7 +246,8 @@ def main():
 
     backend = TimedBackend(batch.DeviceBackend(flt, dev, lanes=args.lanes), torch)
     runner = batch.BatchRunner(backend, rank, world, [n] * nfiles, nch, half, args.normalize,
-                               args.peak_scope, batch.torch_allreduce_max(), lanes=args.lanes)
+                               args.peak_scope, batch.torch_allreduce_max(), lanes=args.lanes,
+                               fuse_normalize=not args.no_fuse_normalize)
     # synthetic samples; configs 4/5 reuse two generated files to bound host time
     cache = {}
 
@@ -379,6 +389,7 @@ def main():
                 "parallelism": f"{world} rank(s), files sharded by batch.plan_shards",
                 "normalize": bool(args.normalize), "peak_scope": args.peak_scope,
                 "peak_exchange": runner.exchange,
+                "fused_normalize": runner.fuse and len(runner.shards) > 1,
                 "lanes": args.lanes,
             },
             "roofline": {

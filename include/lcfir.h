@@ -130,6 +130,23 @@ int lcfir_filter_window_dev(lcfir_ctx *ctx, const float *d_xw, int64_t x_lo, int
                             int64_t y_stride, int64_t start, int64_t end, float *d_peak,
                             int64_t peak_stride, void *stream);
 
+/* lcfir_filter_window_dev that also carries the PREVIOUS file's normalize
+ * (ProcessFile.cp:98-101, applied per file by main.cp:132-147): the ncount
+ * contiguous floats at d_ny are rescaled by 1/peak iff peak = max(d_npeak[0,
+ * nnpeak)) > 1 or nforce -- exactly lcfir_normalize_dev(d_ny, ncount, 1,
+ * ncount, d_npeak, nnpeak, nforce), bit for bit.  The peak slots must be
+ * final when the call's work starts (written by earlier work on `stream`).
+ * For single-partition FFT filters the rescale rides in the filter launch
+ * (the workgroups' older waves do it while waiting at a barrier), so a batch
+ * of files needs one normalize pass (the last file's) instead of one per
+ * file; otherwise it runs as a separate pass after the filter.  d_ny must
+ * not overlap the window or the outputs. */
+int lcfir_filter_window_norm_dev(lcfir_ctx *ctx, const float *d_xw, int64_t x_lo, int64_t x_hi,
+                                 int64_t x_stride, int64_t n, int32_t nch, float *d_yw, int64_t y_lo,
+                                 int64_t y_stride, int64_t start, int64_t end, float *d_peak,
+                                 int64_t peak_stride, float *d_ny, int64_t ncount, const float *d_npeak,
+                                 int32_t nnpeak, int nforce, void *stream);
+
 /* ---- peak + normalize post-pass (ProcessFile.cp:91-101) ----------------- */
 /* max_mag() over each channel (VectorMath::max_mag); d_peak[c] = max(d_peak[c], max|y_c|). */
 int lcfir_peak_reset_dev(float *d_peak, int32_t count, void *stream);

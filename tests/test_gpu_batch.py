@@ -208,3 +208,85 @@ def test_normalize_large_buffer(tt):
         torch.cuda.synchronize()
         ref = (y0.astype(np.float64) * (1.0 / pk)).astype(np.float32)
         assert np.array_equal(view.cpu().numpy(), ref), (n, offset)
+
+
+@pytest.mark.parametrize("kind", ["sym", "general", "parts", "direct"])
+def test_filter_window_norm_matches_separate_passes(tt, oracle_mod, kind):
+    """lcfir_filter_window_norm_dev (a previous file's normalize carried by the
+    filter call; fused into the FFT launch for single-partition filters) is
+    bit-identical to lcfir_filter_window_dev + lcfir_normalize_dev: the call's
+    own outputs and peak, and the rescaled buffer -- for counts of every
+    residue mod 4 (the float4 body and the 1..3-float tail), a peak above 1,
+    a quiet peak with and without force, and a quiet peak left unscaled."""
+    torch, lc = tt
+    import synth
+    rng = np.random.default_rng(11)
+    if kind == "direct":
+        taps, method = oracle_mod.design_lowcut(20.0, 48000.0, 801), "direct"
+    elif kind == "parts":
+        taps, method = oracle_mod.design_lowcut(20.0, 48000.0, 19201), "fft"
+    else:
+        taps, method = oracle_mod.design_lowcut(20.0, 48000.0, 4001), "fft"
+        if kind == "general":
+            taps = taps.copy()
+            taps[7] += 1e-3  # asymmetric: the general (complex) pair table
+    flt = lc.Filter(taps, method=method)
+    n, nch = 150_003, 2
+    x = synth.file_buffer(nch, n, 48000.0, file=3, bits=24)
+    dx = torch.from_numpy(x).cuda()
+    for count, peak_val, force in [(200_000, 1.7, False), (100_001, 0.6, True), (99_998, 0.6, False),
+                                   (77_779, 2.5, True), (4_099, 3.0, False), (3, 1.25, False)]:
+        prev = (rng.standard_normal(count) * 0.3).astype(np.float32)
+        res = []
+        for fused in (False, True):
+            dy = torch.empty((nch, n), dtype=torch.float32, device="cuda")
+            dpk = torch.zeros(1, dtype=torch.float32, device="cuda")
+            dprev = torch.from_numpy(prev.copy()).cuda()
+            dppk = torch.tensor([peak_val], dtype=torch.float32, device="cuda")
+            if fused:
+                flt.filter_window_norm_dev(dx, 0, n, n, n, nch, dy, 0, n, 0, n, dpk, 0, dprev, count,
+                                           dppk, 1, force)
+            else:
+                flt.filter_window_dev(dx, 0, n, n, n, nch, dy, 0, n, 0, n, dpk, peak_stride=0)
+                lc.normalize_dev(dprev, count, 1, count, dppk, 1, force)
+            torch.cuda.synchronize()
+            res.append((dy.cpu().numpy(), dpk.cpu().numpy(), dprev.cpu().numpy()))
+        (y0, p0, r0), (y1, p1, r1) = res
+        assert np.array_equal(y0, y1) and np.array_equal(p0, p1), (kind, count)
+        assert np.array_equal(r0, r1), (kind, count)
+        scaled = peak_val > 1.0 or force
+        want = (prev.astype(np.float64) * (1.0 / np.float64(np.float32(peak_val)))).astype(np.float32) \
+            if scaled else prev
+        assert np.array_equal(r1, want), (kind, count)
+
+
+@pytest.mark.parametrize("lanes,normalize", [(1, True), (1, False), (2, True)])
+def test_batch_runner_fused_normalize_identical(tt, oracle_mod, lanes, normalize):
+    """BatchRunner's fused per-file normalize (each file's rescale carried by
+    the next file's filter launch, the last file's as its own pass) gives the
+    same bytes as the unfused step, over 4 files of ragged lengths with one
+    loud file, every step of a pipelined run."""
+    torch, lc = tt
+    import batch
+    import synth
+    taps = oracle_mod.design_lowcut(20.0, 48000.0, 4001)
+    half = (taps.size - 1) // 2
+    files = [synth.file_buffer(2, 60_001 + 7_777 * f, 48000.0, file=f, bits=24) for f in range(4)]
+    files[1] = (files[1] * np.float32(2.5)).astype(np.float32)
+    flt = lc.Filter(taps, method="fft")
+    outs = []
+    for fuse in (False, True):
+        be = batch.DeviceBackend(flt, torch.device("cuda", 0), lanes=lanes)
+        r = batch.BatchRunner(be, 0, 1, [f.shape[1] for f in files], 2, half, normalize, "file",
+                              lanes=lanes, fuse_normalize=fuse)
+        assert r.fuse == fuse
+        r.prepare(lambda f, lo, hi: files[f][:, lo:hi])
+        got = []
+        for _ in range(2 * lanes + 1):
+            r.step()
+            got.append([(sh.file, y.cpu().numpy(), float(r.peaks[sh.file].item())) for sh, y in r.results()])
+        r.close()
+        outs.append(got)
+    for a, b in zip(*outs):
+        for (fa, ya, pa), (fb, yb, pb) in zip(a, b):
+            assert fa == fb and pa == pb and np.array_equal(ya, yb), fa
