@@ -583,10 +583,10 @@ int lcfir_filter_window_norm_dev(lcfir_ctx *ctx, const float *d_xw, int64_t x_lo
                                  int64_t y_stride, int64_t start, int64_t end, float *d_peak,
                                  int64_t peak_stride, float *d_ny, int64_t ncount, const float *d_npeak,
                                  int32_t nnpeak, int nforce, void *stream) {
-    if (!d_ny || !d_npeak || ncount < 0 || nnpeak < 1) return fail(LCFIR_EINVAL, "bad normalize argument");
-    if (ncount == 0)
+    if (ncount == 0) // nothing to rescale (d_ny and the peak slots may be null)
         return lcfir_filter_window_dev(ctx, d_xw, x_lo, x_hi, x_stride, n, nch, d_yw, y_lo, y_stride, start, end,
                                        d_peak, peak_stride, stream);
+    if (!d_ny || !d_npeak || ncount < 0 || nnpeak < 1) return fail(LCFIR_EINVAL, "bad normalize argument");
     if (!ctx || !d_xw || !d_yw) return fail(LCFIR_EINVAL, "null argument");
     if (nch > 0 && end > start) {
         const size_t xb = sizeof(float) * (size_t)(x_stride * (nch - 1) + (x_hi - x_lo));

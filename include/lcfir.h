@@ -140,7 +140,8 @@ int lcfir_filter_window_dev(lcfir_ctx *ctx, const float *d_xw, int64_t x_lo, int
  * (the workgroups' older waves do it while waiting at a barrier), so a batch
  * of files needs one normalize pass (the last file's) instead of one per
  * file; otherwise it runs as a separate pass after the filter.  d_ny must
- * not overlap the window or the outputs. */
+ * not overlap the window or the outputs; ncount = 0 is a plain
+ * lcfir_filter_window_dev call (d_ny, d_npeak may then be NULL). */
 int lcfir_filter_window_norm_dev(lcfir_ctx *ctx, const float *d_xw, int64_t x_lo, int64_t x_hi,
                                  int64_t x_stride, int64_t n, int32_t nch, float *d_yw, int64_t y_lo,
                                  int64_t y_stride, int64_t start, int64_t end, float *d_peak,

@@ -290,3 +290,47 @@ def test_batch_runner_fused_normalize_identical(tt, oracle_mod, lanes, normalize
     for a, b in zip(*outs):
         for (fa, ya, pa), (fb, yb, pb) in zip(a, b):
             assert fa == fb and pa == pb and np.array_equal(ya, yb), fa
+
+
+def test_filter_window_norm_fallbacks(tt, oracle_mod):
+    """The cases lcfir_filter_window_norm_dev does not fuse still give
+    normalize_dev's bytes: a buffer that is not 16-B aligned, several peak
+    slots (the max is the peak), ncount = 0 (a plain filter call), and a
+    slice too large for one launch's units (a short current file carrying a
+    long previous one).  Bad arguments are rejected."""
+    torch, lc = tt
+    import synth
+    rng = np.random.default_rng(5)
+    flt = lc.Filter(oracle_mod.design_lowcut(20.0, 48000.0, 4001), method="fft")
+    n, nch = 30_001, 1
+    x = synth.file_buffer(nch, n, 48000.0, file=2, bits=24)
+    dx = torch.from_numpy(x).cuda()
+    cases = [(50_001, 1, [1.5]), (40_000, 0, [0.5, 2.25, 1.75]), (0, 0, [3.0]), (3_000_000, 0, [1.5])]
+    for count, offset, peaks in cases:
+        prev = (rng.standard_normal(count + offset) * 0.4).astype(np.float32)
+        res = []
+        for fused in (False, True):
+            dy = torch.empty((nch, n), dtype=torch.float32, device="cuda")
+            dpk = torch.zeros(1, dtype=torch.float32, device="cuda")
+            dprev = torch.from_numpy(prev.copy()).cuda()
+            dppk = torch.tensor(peaks, dtype=torch.float32, device="cuda")
+            view = dprev[offset:]  # offset 1: 4-byte aligned only
+            if fused:
+                flt.filter_window_norm_dev(dx, 0, n, n, n, nch, dy, 0, n, 0, n, dpk, 0, view, count,
+                                           dppk, len(peaks), False)
+            else:
+                flt.filter_window_dev(dx, 0, n, n, n, nch, dy, 0, n, 0, n, dpk, peak_stride=0)
+                if count:
+                    lc.normalize_dev(view, count, 1, count, dppk, len(peaks), False)
+            torch.cuda.synchronize()
+            res.append((dy.cpu().numpy(), dpk.cpu().numpy(), dprev.cpu().numpy()))
+        (y0, p0, r0), (y1, p1, r1) = res
+        assert np.array_equal(y0, y1) and np.array_equal(p0, p1), count
+        assert np.array_equal(r0, r1), count
+    dy = torch.empty((nch, n), dtype=torch.float32, device="cuda")
+    with pytest.raises(lc.LcfirError):  # the rescaled buffer may not overlap the outputs
+        flt.filter_window_norm_dev(dx, 0, n, n, n, nch, dy, 0, n, 0, n, None, 0, dy, n,
+                                   torch.ones(1, device="cuda"), 1, True)
+    with pytest.raises(lc.LcfirError):  # at least one peak slot
+        flt.filter_window_norm_dev(dx, 0, n, n, n, nch, dy, 0, n, 0, n, None, 0, dx, n,
+                                   torch.ones(1, device="cuda"), 0, True)
