@@ -263,12 +263,21 @@ def main():
     # Pre-roll: untimed steps until the shader clock has settled.  Back-to-back
     # launches ramp it over the first few hundred ms (a 20-step
     # region right after 5 warmup steps measured 8-20 % below steady state).
+    # Every rank must run the same number of steps (a step with a peak
+    # exchange is a collective): the ranks agree after each batch of 8, and
+    # stop as soon as any rank's clock has run out.
     preroll_steps, t_pre = 0, time.perf_counter()
-    while time.perf_counter() - t_pre < args.preroll_s:
+    more = args.preroll_s > 0
+    while more:
         for _ in range(8):
             runner.step()
         preroll_steps += 8
         torch.cuda.synchronize(dev)
+        more = time.perf_counter() - t_pre < args.preroll_s
+        if world > 1:
+            flag = torch.tensor([1 if more else 0], dtype=torch.int32, device=dev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            more = bool(flag.item())
     preroll_s = time.perf_counter() - t_pre
     # The dominant kernel's exclusive time: the same filter launches, one
     # stream, nothing else in flight (HIP events on that stream), right after
