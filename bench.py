@@ -204,6 +204,25 @@ class TimedBackend:
         return self._timed(self.inner.filter_normalize_prev, *a, **k)
 
 
+def preroll(step, seconds, sync, agree=None, batch=8):
+    """Untimed steps, in batches, until `seconds` have passed.  Every rank
+    must run the same number of steps (a step with a peak exchange is a
+    collective), so with `agree` (a MIN all-reduce of the continue flag) the
+    ranks decide together after each batch and stop as soon as any rank's
+    clock has run out.  Returns the step count."""
+    steps, t0 = 0, time.perf_counter()
+    more = seconds > 0
+    while more:
+        for _ in range(batch):
+            step()
+        steps += batch
+        sync()
+        more = time.perf_counter() - t0 < seconds
+        if agree is not None:
+            more = agree(more)
+    return steps
+
+
 def main():
     args = parse()
     import numpy as np
@@ -263,21 +282,14 @@ def main():
     # Pre-roll: untimed steps until the shader clock has settled.  Back-to-back
     # launches ramp it over the first few hundred ms (a 20-step
     # region right after 5 warmup steps measured 8-20 % below steady state).
-    # Every rank must run the same number of steps (a step with a peak
-    # exchange is a collective): the ranks agree after each batch of 8, and
-    # stop as soon as any rank's clock has run out.
-    preroll_steps, t_pre = 0, time.perf_counter()
-    more = args.preroll_s > 0
-    while more:
-        for _ in range(8):
-            runner.step()
-        preroll_steps += 8
-        torch.cuda.synchronize(dev)
-        more = time.perf_counter() - t_pre < args.preroll_s
-        if world > 1:
-            flag = torch.tensor([1 if more else 0], dtype=torch.int32, device=dev)
-            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-            more = bool(flag.item())
+    def agree(more):
+        flag = torch.tensor([1 if more else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        return bool(flag.item())
+
+    t_pre = time.perf_counter()
+    preroll_steps = preroll(runner.step, args.preroll_s, lambda: torch.cuda.synchronize(dev),
+                            agree if world > 1 else None)
     preroll_s = time.perf_counter() - t_pre
     # The dominant kernel's exclusive time: the same filter launches, one
     # stream, nothing else in flight (HIP events on that stream), right after

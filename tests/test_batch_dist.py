@@ -220,3 +220,51 @@ def test_batch_lanes_pipeline(lanes, normalize):
     assert len(set().union(*outs_by_lane.values())) == nfiles * lanes
     with pytest.raises(ValueError):
         batch.BatchRunner(be, 0, 1, [n], nch, HALF, lanes=0)
+
+
+def _preroll_worker(rank, world, port, q):
+    import time
+    import torch
+    import sys
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+
+    def step():  # a step with a peak exchange: a collective, slower on rank 1
+        t = torch.zeros(1)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        time.sleep(0.002 * (1 + 3 * rank))
+
+    def agree(more):
+        flag = torch.tensor([1 if more else 0], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        return bool(flag.item())
+
+    t0 = time.perf_counter()
+    # rank 1's clock runs out first (a shorter budget): without the agreement
+    # rank 0 would go on stepping into a collective rank 1 never joins
+    n = bench.preroll(step, 0.25 if rank == 0 else 0.1, lambda: None, agree)
+    dist.barrier()
+    q.put((rank, n, time.perf_counter() - t0))
+    dist.destroy_process_group()
+
+
+def test_bench_preroll_agrees_across_ranks():
+    """bench.py's pre-roll is time-based; with a peak exchange every step is a
+    collective, so the ranks must run the same number of steps.  preroll()
+    lets them agree after every batch (gloo, world 2, different budgets and
+    step times): same count on both ranks, no deadlock."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_preroll_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got[0][1] == got[1][1] and got[0][1] % 8 == 0 and got[0][1] >= 8
