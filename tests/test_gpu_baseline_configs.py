@@ -2,7 +2,8 @@
 
   * config 2 (10 min stereo 48 kHz int24, 4001 taps): EVERY one of the 57.6 M
     outputs against the oracle's strict-order f64 FMA restatement of
-    FilterCore.h:56-76, run multithreaded on the box's cores (~12 s).  Bars:
+    FilterCore.h:56-76, run multithreaded on the box's cores (~12 s).
+    Config 3 (8-ch 96 kHz f32, 8001 taps) the same way, all 46.1 M outputs.  Bars:
     direct method bit-exact; FFT within 1 f32 ulp of it everywhere, RMS vs the
     long-double oracle <= 1e-9, and every FFT/FMA difference an output whose
     long-double value is within 1 ulp too (f32 rounding of values the two f64
@@ -96,6 +97,53 @@ def test_config2_every_sample(tt, oracle_mod, config2, method):
         if diff.size:
             ld_all, _ = oracle_mod.filter_points(x[c], taps, diff, oracle_mod.MODE_LD)
             d[diff] = y[c][diff].astype(np.float64) - ld_all.astype(np.float64)
+        assert np.sqrt(np.mean(d * d)) <= RMS_TOL
+
+
+@pytest.fixture(scope="module")
+def config3(oracle_mod):
+    import synth
+    fs, n, nch = 96000.0, 5_760_000, 8
+    taps = oracle_mod.design_lowcut(20.0, fs, 8001)
+    x = synth.file_buffer(nch, n, fs, file=3, bits=None)  # float32 source
+    ref = np.stack([oracle_mod.filter_channel_mt(x[c], taps, _cores(), oracle_mod.MODE_FMA)
+                    for c in range(nch)])
+    return x, taps, ref
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("method", ["direct", "fft"])
+def test_config3_every_sample(tt, oracle_mod, config3, method):
+    """Config 3 (60 s of 8-channel 96 kHz float32, 8001 taps): every one of
+    the 46.1 M outputs, with config 2's bars (direct bit-exact against the
+    FMA chain; FFT within 1 ulp of it, every difference within 1 ulp of the
+    long-double value, RMS <= 1e-9) and the fused per-channel peaks."""
+    torch, lc = tt
+    x, taps, ref = config3
+    nch, n = x.shape
+    flt = lc.Filter(taps, method=method)
+    xd = torch.from_numpy(x).cuda()
+    yd = torch.empty_like(xd)
+    pk = torch.zeros(nch, dtype=torch.float32, device="cuda")
+    flt.filter_channels_dev(xd, n, nch, n, yd, n, pk)
+    torch.cuda.synchronize()
+    y = yd.cpu().numpy()
+    peaks = pk.cpu().numpy()
+    del xd, yd
+    for c in range(nch):
+        assert np.isfinite(y[c]).all()
+        assert peaks[c] == np.abs(y[c]).max()
+        if method == "direct":
+            assert np.array_equal(y[c], ref[c])
+            continue
+        u = _ulps(y[c], ref[c])
+        assert u.max() <= 1
+        diff = np.nonzero(u)[0]
+        d = y[c].astype(np.float64) - ref[c].astype(np.float64)
+        if diff.size:
+            ld, _ = oracle_mod.filter_points(x[c], taps, diff, oracle_mod.MODE_LD)
+            assert _ulps(y[c][diff], ld).max() <= 1
+            d[diff] = y[c][diff].astype(np.float64) - ld.astype(np.float64)
         assert np.sqrt(np.mean(d * d)) <= RMS_TOL
 
 
