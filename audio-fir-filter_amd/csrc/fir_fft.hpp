@@ -876,8 +876,9 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     //   conj(V_k) = conj(Z_k P1 + conj(Z_{M-k}) P2),  conj(V_{M-k}) = conj(Z_{M-k}) Q2 - Z_k P2
     // with S = G_k + conj(G_{M-k}), D = G_k - conj(G_{M-k}), W = W_L^k:
     //   P1 = 2 (S + D Im W),  P2 = 2i D Re W,  Q2 = 2 (S - D Im W)
-    // The table holds 2S and 2D per (slot, thread) (host, long double); W comes
-    // from one per-thread base times W_16^i.
+    // General form: the table holds 2S and 2D per (slot, thread) (host, long
+    // double) and W comes from one per-thread base times W_16^i.  Zero-phase
+    // form: the table holds P1 = p1, Q2 = q2 and P2 / i = p2 per bin.
     {
         // Wave 0 (a scalar, wave-uniform branch) permutes its special lane
         // into the generic layout first (fft_w0_permute_in).
@@ -1186,7 +1187,8 @@ inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, hipSt
     // pair tables in consumption order: slot i of thread t holds bin k_i of
     // its task A (special lane: the permuted list; slot 8: k = M/2) as the
     // collapsed split/multiply/merge coefficients 2S, 2D, plus W_L^k in the
-    // third field (the kernel reads slot 0's as its W base)
+    // third field (the kernel reads slot 0's as its W base); the zero-phase
+    // form stores fft_pair_sym's p1, q2, p2 per bin instead (kFftSymPQ, kFftSymP2)
     std::vector<double2> pair((size_t)parts * kFftPairTable);
     std::vector<uint32_t> task((size_t)kFftNT);
     std::vector<double2> c8((size_t)parts);

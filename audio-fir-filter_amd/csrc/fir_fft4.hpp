@@ -107,7 +107,7 @@ __device__ __forceinline__ float fft4_store(const DirectParams &p, const double2
     return pk;
 }
 
-// Pair-table registers of one half: the real (2S, 2D) per slot in zero-phase
+// Pair-table registers of one half: the real p1, q2, p2 per slot in zero-phase
 // form, complex 2S and 2D otherwise, plus the W_L^k base of slot 0.
 template <int kOut>
 struct Fft4Pair {
