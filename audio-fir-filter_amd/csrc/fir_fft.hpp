@@ -801,6 +801,11 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
 #pragma unroll
     for (int t = 0; t < 8; ++t) x1[t] = blk1[lane + 64 * t];
     powers8(twl[512 + lane], tws);
+    double2 tws_a[8]; // W_512^(lane r): stage A' of task A needs the same powers (waves 1..7, wave 0 lanes < 32)
+    if constexpr (kOut == kFftOutSym) {
+#pragma unroll
+        for (int r = 1; r < 8; ++r) tws_a[r] = tws[r];
+    }
     dft8(x0);
     twiddle8(x0, tws);
 #pragma unroll
@@ -918,7 +923,18 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     // ---- inverse stage A': per task radix-8 over e2 -> beta0; * W_512^(beta0 d')
     {
         double2 *ba = flds + 512 * cA, *bb = flds + 512 * cB;
-        powers8(twl[512 + dA + 8 * eA], tws);
+        if constexpr (kOut == kFftOutSym) {
+            // task A's d' = dA + 8 eA is the lane except in wave 0's column-0
+            // lanes (kFftWave0C0): a wave-uniform choice
+            if (__builtin_amdgcn_readfirstlane(w) != 0) {
+#pragma unroll
+                for (int r = 1; r < 8; ++r) tws[r] = tws_a[r];
+            } else {
+                powers8(twl[512 + dA + 8 * eA], tws);
+            }
+        } else {
+            powers8(twl[512 + dA + 8 * eA], tws);
+        }
         dft8(x0);
         twiddle8(x0, tws);
 #pragma unroll
