@@ -64,6 +64,12 @@ def main():
             "per_file": [{"file": f, "read_s": float(rd), "gpu_s": float(g), "write_s": float(w)}
                          for f, rd, g, w in per_file],
         }
+        # steady state: the pipeline's slowest stage per file, after the first
+        # file (which also pays the ctx, FFT plan and buffer set-up)
+        later = sorted(max(float(rd), float(g), float(w)) for _, rd, g, w in per_file[1:])
+        if later:
+            res["steady_stage_s"] = later[len(later) // 2]
+            res["steady_msamples_per_s"] = nch * n / res["steady_stage_s"] / 1e6
         os.makedirs(os.path.dirname(a.out), exist_ok=True)
         with open(a.out, "w") as fh:
             json.dump(res, fh, indent=1)
