@@ -9,14 +9,26 @@ both methods.  Every case against the oracle at sampled positions:
   * sub-ranges computed from only their input window equal to the same
     outputs of the whole-channel call (bit for bit, same method);
   * the fused per-channel peak equal to max |y| of the whole channel.
+
+A second set fuzzes lcfir_filter_window_norm_dev (a previous file's normalize
+carried by the filter call) against the separate filter + normalize calls.
+
+LCFIR_FUZZ_CASES / LCFIR_FUZZ_NORM_CASES / LCFIR_FUZZ_SEED0 widen or shift the
+seed range for a longer campaign (scripts/gpu_fuzz.sh); the defaults are the
+round-end suite's.
 """
+import os
+
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
 
 RMS_TOL = 1e-9
-N_CASES = 120
+SEED0 = int(os.environ.get("LCFIR_FUZZ_SEED0", "0"))
+N_CASES = int(os.environ.get("LCFIR_FUZZ_CASES", "120"))
+N_NORM_CASES = int(os.environ.get("LCFIR_FUZZ_NORM_CASES", "40"))
+NRM_SLICE_MAX = 14 * 1024  # floats of the previous buffer one FFT unit rescales (fir_fft.hpp kNrmK)
 
 
 def _max_ulps(a, b, floor=1e-12):
@@ -44,7 +56,7 @@ def _case(seed):
     return rng, ntaps, nch, max(1, n), method, designed
 
 
-@pytest.mark.parametrize("seed", range(N_CASES))
+@pytest.mark.parametrize("seed", range(SEED0, SEED0 + N_CASES))
 def test_random_case(oracle_mod, seed):
     import lcfir as lc
     rng, ntaps, nch, n, method, designed = _case(seed)
@@ -99,3 +111,76 @@ def test_random_case(oracle_mod, seed):
         dxw.free()
         dyw.free()
         assert np.array_equal(yw, y[:, start:end]), (seed, start, end)
+
+
+def _norm_case(seed):
+    rng = np.random.default_rng(5000 + seed)
+    ntaps = int(rng.choice([401, 1601, 4001, 4001, 4003, 8001, 10925, 19201]))
+    method = "direct" if ntaps <= 1601 and rng.random() < 0.3 else "fft"
+    nch = int(rng.integers(1, 4))
+    n = int(rng.choice([1, 7, ntaps // 2 + 1, 20_000, 123_457, 300_001]))
+    # units of a one-partition FFT launch (B = L - T + 1, L = 16384; 19 201
+    # taps run as 2 x 9 601): counts around units * 14 Ki floats straddle the
+    # fused / separate-pass switch
+    B = 16384 - (ntaps if ntaps <= 10925 else 9601) + 1
+    boundary = -(-n // B) * nch * NRM_SLICE_MAX
+    count = int(rng.choice([
+        1, 3, int(rng.integers(1, 5_000)), int(rng.integers(1, boundary + 1)),
+        int(rng.integers(1, boundary + 1)), boundary, boundary + int(rng.integers(-8, 9)),
+        int(rng.integers(boundary, 2 * boundary + 1))]))
+    if rng.random() < 0.05:
+        count = 0  # a plain filter call
+    offset = int(rng.choice([0, 0, 0, 0, 0, 1, 2, 3, 4]))  # floats: 16-B aligned when offset % 4 == 0
+    npeak = int(rng.integers(1, 4))
+    peaks = rng.choice([0.0, 0.25, 0.999, 1.0, 1.0000001, 1.5, 3.0], npeak).astype(np.float32)
+    if rng.random() < 0.5:
+        peaks[int(rng.integers(npeak))] = np.float32(rng.uniform(0.01, 4.0))
+    force = bool(rng.random() < 0.4)
+    designed = rng.random() < 0.6
+    return rng, ntaps, method, nch, n, count, offset, peaks, force, designed
+
+
+@pytest.mark.parametrize("seed", range(SEED0, SEED0 + N_NORM_CASES))
+def test_random_norm_case(oracle_mod, seed):
+    """filter + previous-buffer rescale in one call (fused into the FFT launch
+    where fft_nrm_fusable, else its own pass) equals the two separate calls
+    byte for byte: the filter's outputs and peak, and the rescaled buffer,
+    which also equals (float)((double)v * (1 / max(peaks))) under the
+    ProcessFile.cp:98-101 decision."""
+    import torch  # before lcfir: one HIP runtime in the process
+    import lcfir as lc
+    rng, ntaps, method, nch, n, count, offset, peaks, force, designed = _norm_case(seed)
+    if designed:
+        taps = oracle_mod.design_lowcut(float(rng.uniform(5.0, 300.0)), 48000.0, ntaps)
+    else:
+        taps = rng.standard_normal(ntaps) / np.sqrt(ntaps)
+    x = np.ascontiguousarray(np.rint(rng.uniform(-0.9, 0.9, (nch, n)) * 2 ** 23) / 2 ** 23, np.float32)
+    prev = (rng.standard_normal(count + offset) * 0.5).astype(np.float32)
+    flt = lc.Filter(taps, method=method)
+    dx = torch.from_numpy(x).cuda()
+    res = []
+    for fused in (False, True):
+        dy = torch.empty((nch, n), dtype=torch.float32, device="cuda")
+        dpk = torch.zeros(1, dtype=torch.float32, device="cuda")
+        dprev = torch.from_numpy(prev.copy()).cuda()
+        dppk = torch.from_numpy(peaks.copy()).cuda()
+        view = dprev[offset:]
+        if fused:
+            flt.filter_window_norm_dev(dx, 0, n, n, n, nch, dy, 0, n, 0, n, dpk, 0, view, count,
+                                       dppk, peaks.size, force)
+        else:
+            flt.filter_window_dev(dx, 0, n, n, n, nch, dy, 0, n, 0, n, dpk, peak_stride=0)
+            if count:
+                lc.normalize_dev(view, count, 1, count, dppk, peaks.size, force)
+        torch.cuda.synchronize()
+        res.append((dy.cpu().numpy(), dpk.cpu().numpy(), dprev.cpu().numpy()))
+    (y0, p0, r0), (y1, p1, r1) = res
+    case = (seed, ntaps, method, nch, n, count, offset, peaks.tolist(), force)
+    assert np.array_equal(y0, y1) and np.array_equal(p0, p1), case
+    assert np.array_equal(r0, r1), case
+    pk = np.float32(peaks.max())
+    body = prev[offset:]
+    if (pk > 1.0 or force) and pk > 0.0:
+        body = (body.astype(np.float64) * (1.0 / np.float64(pk))).astype(np.float32)
+    assert np.array_equal(r1[offset:], body) and np.array_equal(r1[:offset], prev[:offset]), case
+    assert p1[0] == np.abs(y1).max(), case
