@@ -89,6 +89,10 @@ class Backend:
     def alloc_out(self, nch: int, count: int):  # -> handle
         raise NotImplementedError
 
+    def window(self, n: int, start: int, end: int, half: int):
+        """Input samples [x_lo, x_hi) to read for outputs [start, end)."""
+        return window(Shard(-1, start, end), n, half)
+
     def filter(self, xw, x_lo, x_hi, n, nch, yw, start, end, peaks, slot: int):
         """outputs [start, end) into yw; max|y| over the shard's channels into peaks[slot]."""
         raise NotImplementedError
@@ -196,7 +200,7 @@ class BatchRunner:
                 self.b.zero_peaks(pk)
         for sh in self.shards:
             n = self.nframes[sh.file]
-            lo, hi = window(sh, n, self.half)
+            lo, hi = self.b.window(n, sh.start, sh.end, self.half)
             xw = self.b.upload(sh.file, get_window(sh.file, lo, hi), lo, hi)
             self.inputs.append((xw, lo, hi))
             for lane, outs in enumerate(self._outs):
@@ -311,6 +315,11 @@ class DeviceBackend(Backend):
 
     def alloc_out(self, nch, count):
         return self.torch.empty((nch, count), dtype=self.torch.float32, device=self.dev)
+
+    def window(self, n, start, end, half):
+        # the whole segments the FFT's units read: a split file's outputs are
+        # then bit-identical to the unsplit file's (lcfir_ctx_window)
+        return self.flt.window(n, start, end)
 
     def zero_peaks(self, peaks):
         self.lc.peak_reset_dev(peaks, peaks.numel(), self.sp)

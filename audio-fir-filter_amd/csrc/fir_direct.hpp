@@ -42,6 +42,7 @@ struct DirectParams {
     int32_t ntaps;
     int32_t half;
     int64_t start, end; // output range (global indices)
+    int64_t seg0;       // FFT only: first output of the launch's first segment (<= start; fft_launch_group)
     int32_t tc;         // taps per LDS stage (multiple of 2R)
     unsigned *peak;     // max|y| as float bits (nullable): channel c -> peak[c * peak_stride]
     int64_t peak_stride;

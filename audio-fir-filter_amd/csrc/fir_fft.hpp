@@ -729,7 +729,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     {
         const int u = fft_unit32(0, blockIdx.x, gridDim.x, gd.units); // < units: the grid is <= units
         const int c = fft_div(u, gd);
-        fft_load_unit(p, c, p.start + (int64_t)(u - c * gd.nseg) * B, threadIdx.x, v);
+        fft_load_unit(p, c, p.seg0 + (int64_t)(u - c * gd.nseg) * B, threadIdx.x, v);
     }
     // vmcnt counts loads and stores together, in issue order, and the wait
     // pass merges the loop's entry and back edge path-insensitively.  Both
@@ -760,7 +760,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     double2 *blk0 = flds + 512 * (2 * w);
     double2 *blk1 = blk0 + 512;
     const int ch = fft_div(u, gd);
-    const int64_t n0 = p.start + (int64_t)(u - ch * gd.nseg) * B;
+    const int64_t n0 = p.seg0 + (int64_t)(u - ch * gd.nseg) * B;
     FFT_STAMP(0);
     FFT_USTAMP(1 + rnd);
 
@@ -917,7 +917,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
         const int un1 = fft_unit32(rnd + 1, blockIdx.x, gridDim.x, gd.units);
         const int un = un1 < gd.units ? un1 : u;
         const int cn = fft_div(un, gd);
-        fft_load_unit(p, cn, p.start + (int64_t)(un - cn * gd.nseg) * B, j, v);
+        fft_load_unit(p, cn, p.seg0 + (int64_t)(un - cn * gd.nseg) * B, j, v);
     }
 
     // ---- inverse stage A': per task radix-8 over e2 -> beta0; * W_512^(beta0 d')
@@ -1040,12 +1040,14 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     // L - half) for the zero-phase one (kSym: half even, fft_plan_build)
     const int cmin = kSym ? p.half : p.ntaps - 1;
     const int cmax = kSym ? kFftL - p.half : kFftL;
+    // (negative for outputs before `start`: the launch's segment grid starts
+    // at p.seg0 <= start, fft_launch_group)
     const int64_t off = n0 - cmin - p.start; // offset (samples) of c[0] from start
     const int64_t oend = p.end - p.start;
     float pk = 0.0f;
     if constexpr (kOut == kFftOutF32 || kSym) {
-    if (n0 + B <= p.end) {
-        // every output of this unit is before `end`: the pair (c, c+1) is
+    if (n0 >= p.start && n0 + B <= p.end) {
+        // every output of this unit is in [start, end): the pair (c, c+1) is
         // valid iff cmin <= c < cmax (cmin, cmax and o are even), so both
         // stores share one offset and may merge into a dwordx2.  (A resource
         // over the unit's B outputs, letting the range check drop the rest,
@@ -1068,7 +1070,8 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
             const int c = 2 * (j + 512 * r);
             const float f0 = (float)a[r].x, f1 = (float)(-a[r].y);
             const int64_t o = off + c;
-            const bool ok0 = c >= cmin && c < cmax && o < oend, ok1 = c + 1 >= cmin && c + 1 < cmax && o + 1 < oend;
+            const bool ok0 = c >= cmin && c < cmax && o >= 0 && o < oend,
+                       ok1 = c + 1 >= cmin && c + 1 < cmax && o + 1 >= 0 && o + 1 < oend;
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(f0), ys,
                                                   ok0 ? (int)(o * 4) : (int)0x80000000, 0, kNtStore);
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(f1), ys,
@@ -1089,7 +1092,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
         for (int r = 0; r < 16; ++r) {
             const int c = 2 * (j + 512 * r);
             const int64_t o = off + c;
-            const bool ok0 = c >= cmin && o < oend, ok1 = c + 1 >= cmin && o + 1 < oend;
+            const bool ok0 = c >= cmin && o >= 0 && o < oend, ok1 = c + 1 >= cmin && o + 1 >= 0 && o + 1 < oend;
             const int oz0 = ok0 ? (int)(o * 8) : (int)0x80000000;
             const int oz1 = ok1 ? (int)(o * 8 + 8) : (int)0x80000000;
             double v0 = a[r].x, v1 = -a[r].y;
@@ -1369,7 +1372,7 @@ inline bool fft_launch_one(const FftPlan &plan, const DirectParams &q, int part,
                                    (int)fft_lds_bytes()) == hipSuccess;
     }();
     (void)attr;
-    const int64_t nseg = (q.end - q.start + plan.B - 1) / plan.B;
+    const int64_t nseg = (q.end - q.seg0 + plan.B - 1) / plan.B;
     const int64_t units = nseg * nch; // < 2^31 (fft_launch)
     const int64_t grid = std::min<int64_t>(units, (int64_t)plan.cus * fft_blocks_per_cu());
     const FftGrid gd = fft_grid(nseg, units);
@@ -1407,7 +1410,7 @@ inline bool fft16_launch(const FftPlan &plan, const DirectParams &q, int nch, hi
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)fft16_lds_bytes()) == hipSuccess;
     }();
     (void)attr;
-    const int64_t nseg = (q.end - q.start + plan.B - 1) / plan.B;
+    const int64_t nseg = (q.end - q.seg0 + plan.B - 1) / plan.B;
     const int64_t units = nseg * nch; // < 2^31 (fft_launch)
     const int64_t grid = std::min<int64_t>(units, (int64_t)plan.cus);
     hipLaunchKernelGGL(fir_fft16_f64_kernel<kFftOutSym>, dim3((unsigned)grid), dim3(kFft16NT), fft16_lds_bytes(), s, q,
@@ -1425,11 +1428,39 @@ inline bool fft16_launch(const FftPlan &plan, const DirectParams &q, int nch, hi
 inline int64_t fft_chunk_outputs(const FftPlan &plan) {
     return plan.parts == 1 ? fft_chunk() : std::min<int64_t>(fft_chunk(), (int64_t)1 << 26);
 }
+// The segment grid is anchored at output 0 of the channel: segment s covers
+// outputs [s B, (s + 1) B) whatever range a call asks for, and launch chunks
+// are whole segments.  A unit's outputs depend only on the samples it reads,
+// so every output comes out the same, bit for bit, from any call whose input
+// window holds its unit's samples (fft_window): the whole-channel call,
+// windowed calls over any sub-range, chunked launches and channel groups all
+// agree.  That is FilterCore.h's partition invariance -- ProcessFile.cp:60-83
+// splits a channel into per-thread ranges and the result does not depend on
+// how -- kept by the FFT method.  A range that starts inside a segment pays
+// for that whole segment (at most one extra unit per channel and call).
+inline int64_t fft_grid_start(const FftPlan &plan, int64_t start) { return start - start % plan.B; }
+inline int64_t fft_chunk_span(const FftPlan &plan) {
+    return std::max<int64_t>(plan.B, fft_chunk_outputs(plan) / plan.B * plan.B);
+}
+// Input samples [lo, hi) the units of outputs [start, end) read (unclipped;
+// samples outside the channel are zeros to every unit alike).  Segment n0 of
+// partition k reads x[n0 - half + k ntaps_k + i], i < L.
+inline void fft_window(const FftPlan &plan, int64_t half, int64_t start, int64_t end, int64_t &lo, int64_t &hi) {
+    const int64_t g0 = fft_grid_start(plan, start);
+    const int64_t last = g0 + std::max<int64_t>(0, (end - g0 + plan.B - 1) / plan.B - 1) * plan.B;
+    lo = g0 - half;
+    hi = last - half + (int64_t)(plan.parts - 1) * plan.ntaps + kFftL;
+}
+// Segments of the first launch chunk of [p.start, p.end)
+inline int64_t fft_first_nseg(const FftPlan &plan, const DirectParams &p) {
+    const int64_t g0 = fft_grid_start(plan, p.start);
+    return (std::min(p.end - g0, fft_chunk_span(plan)) + plan.B - 1) / plan.B;
+}
 // Doubles of partial-sum scratch one fft_launch of p over nch channels needs
 // (0 for a single-partition filter); the chunks reuse it in stream order.
 inline size_t fft_scratch_doubles(const FftPlan &plan, const DirectParams &p, int nch) {
     if (plan.parts == 1 || p.end <= p.start) return 0;
-    return (size_t)std::min<int64_t>(p.end - p.start, fft_chunk_outputs(plan)) * (size_t)std::max(nch, 1);
+    return (size_t)std::min<int64_t>(p.end - p.start, fft_chunk_span(plan)) * (size_t)std::max(nch, 1);
 }
 
 // Filter outputs [p.start, p.end) of nch channels.  p.half / p.ntaps are the
@@ -1457,7 +1488,7 @@ inline bool fft_nrm_fusable(const FftPlan &plan, const FftNrm &nrm, const Direct
     if (plan.parts != 1 || plan.waves16 || fft_use_w4() || !nrm.y || !nrm.peak || nrm.npeak < 1 ||
         (reinterpret_cast<uintptr_t>(nrm.y) & 15) != 0 || p.end <= p.start || nch <= 0)
         return false;
-    const int64_t nseg = (std::min(p.end - p.start, fft_chunk_outputs(plan)) + plan.B - 1) / plan.B;
+    const int64_t nseg = fft_first_nseg(plan, p);
     const int64_t group = std::max<int64_t>(1, std::min<int64_t>(nch, fft_max_units() / nseg));
     const int64_t units = nseg * group;
     const int64_t per = (nrm.count + units - 1) / units;
@@ -1478,7 +1509,7 @@ inline bool fft_launch(const FftPlan &plan, const DirectParams &p, int nch, hipS
     // the kernels index units in 32 bits (FftGrid): channel groups keep every
     // launch's channels x segments below 2^31 (the partial-sum scratch is
     // reused by each group in stream order)
-    const int64_t nseg = (std::min(p.end - p.start, fft_chunk_outputs(plan)) + plan.B - 1) / plan.B;
+    const int64_t nseg = fft_first_nseg(plan, p);
     const int group = (int)std::max<int64_t>(1, std::min<int64_t>(nch, fft_max_units() / nseg));
     for (int c0 = 0; c0 < nch; c0 += group) {
         DirectParams q = p;
@@ -1491,14 +1522,18 @@ inline bool fft_launch(const FftPlan &plan, const DirectParams &p, int nch, hipS
 }
 inline bool fft_launch_group(const FftPlan &plan, const DirectParams &p, int nch, hipStream_t s,
                              std::string &err, const FftNrm *nrm) {
-    const int64_t chunk = fft_chunk_outputs(plan);
-    for (int64_t cs = p.start; cs < p.end; cs += chunk) {
+    const int64_t span = fft_chunk_span(plan);
+    const int64_t g0 = fft_grid_start(plan, p.start);
+    for (int64_t cs = g0; cs < p.end; cs += span) {
         DirectParams q = p;
-        q.start = cs;
-        q.end = std::min(p.end, cs + chunk);
-        // every partition reads inside x[start - half, end - half + T - 1)
-        const int64_t lo = std::max(p.x_lo, q.start - p.half);
-        const int64_t hi = std::max(lo, std::min(p.x_hi, q.end - p.half + p.ntaps - 1));
+        q.seg0 = cs;
+        q.start = std::max(cs, p.start);
+        q.end = std::min(p.end, cs + span);
+        // every partition of every unit reads inside fft_window
+        int64_t wlo, whi;
+        fft_window(plan, p.half, q.start, q.end, wlo, whi);
+        const int64_t lo = std::max(p.x_lo, wlo);
+        const int64_t hi = std::max(lo, std::min(p.x_hi, whi));
         q.x = p.x + (lo - p.x_lo);
         q.x_lo = lo;
         q.x_hi = hi;
@@ -1509,7 +1544,7 @@ inline bool fft_launch_group(const FftPlan &plan, const DirectParams &p, int nch
                 continue;
             }
             // the first chunk's launch carries the fused normalize
-            const bool fuse = nrm && cs == p.start;
+            const bool fuse = nrm && cs == g0;
             bool ok;
             if (plan.sym)
                 ok = fuse ? fft_launch_one<kFftOutSym, true>(plan, q, 0, nch, s, err, *nrm)

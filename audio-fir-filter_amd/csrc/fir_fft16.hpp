@@ -153,7 +153,7 @@ __global__ __launch_bounds__(kFft16NT) void fir_fft16_f64_kernel(DirectParams p,
     {
         const int u = fft_unit32(0, blockIdx.x, gridDim.x, gd.units);
         const int c0 = fft_div(u, gd);
-        fft16_load_unit(p, c0, p.start + (int64_t)(u - c0 * gd.nseg) * B, m0, v);
+        fft16_load_unit(p, c0, p.seg0 + (int64_t)(u - c0 * gd.nseg) * B, m0, v);
     }
     __builtin_amdgcn_s_waitcnt(kVmcnt0);
     __syncthreads();
@@ -166,7 +166,7 @@ __global__ __launch_bounds__(kFft16NT) void fir_fft16_f64_kernel(DirectParams p,
          u = fft_unit32(++rnd, blockIdx.x, gridDim.x, gd.units)) {
     const int par = (int)(rnd & 1);
     const int ch = fft_div(u, gd);
-    const int64_t n0 = p.start + (int64_t)(u - ch * gd.nseg) * B;
+    const int64_t n0 = p.seg0 + (int64_t)(u - ch * gd.nseg) * B;
 
     // ---- stage 1: lane pair (b, h): 8-point DFT over a' -> swap -> radix-2
     {
@@ -251,7 +251,7 @@ __global__ __launch_bounds__(kFft16NT) void fir_fft16_f64_kernel(DirectParams p,
         const int un1 = fft_unit32(rnd + 1, blockIdx.x, gridDim.x, gd.units);
         const int un = un1 < gd.units ? un1 : u;
         const int cn = fft_div(un, gd);
-        fft16_load_unit(p, cn, p.start + (int64_t)(un - cn * gd.nseg) * B, m0, v);
+        fft16_load_unit(p, cn, p.seg0 + (int64_t)(un - cn * gd.nseg) * B, m0, v);
     }
     // ---- inverse stage A' (task d' = lane): radix-8 over e2 -> beta0; * W_512^(beta0 lane)
     // in the partner's block: this wave has read it, and only this wave reads it
@@ -303,7 +303,7 @@ __global__ __launch_bounds__(kFft16NT) void fir_fft16_f64_kernel(DirectParams p,
     const int64_t off = n0 - cmin - p.start;
     const int64_t oend = p.end - p.start;
     float pk = 0.0f;
-    if (n0 + B <= p.end) {
+    if (n0 >= p.start && n0 + B <= p.end) {
 #pragma unroll
         for (int a = 0; a < 8; ++a) {
             const int c = 2 * (512 * (2 * a + hh) + b);
@@ -320,7 +320,8 @@ __global__ __launch_bounds__(kFft16NT) void fir_fft16_f64_kernel(DirectParams p,
             const int c = 2 * (512 * (2 * a + hh) + b);
             const float f0 = (float)r[a].x, f1 = (float)(-r[a].y);
             const int64_t o = off + c;
-            const bool ok0 = c >= cmin && c < cmax && o < oend, ok1 = c + 1 >= cmin && c + 1 < cmax && o + 1 < oend;
+            const bool ok0 = c >= cmin && c < cmax && o >= 0 && o < oend,
+                       ok1 = c + 1 >= cmin && c + 1 < cmax && o + 1 >= 0 && o + 1 < oend;
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(f0), ys, ok0 ? (int)(o * 4) : (int)0x80000000, 0,
                                                   kNtStore);
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(f1), ys, ok1 ? (int)(o * 4 + 4) : (int)0x80000000,

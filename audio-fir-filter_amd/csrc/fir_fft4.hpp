@@ -49,7 +49,7 @@ __device__ __forceinline__ float fft4_store(const DirectParams &p, const double2
     const int64_t oend = p.end - p.start;
     float pk = 0.0f;
     if constexpr (kOut == kFftOutF32 || kSym) {
-        if (n0 + B <= p.end) {
+        if (n0 >= p.start && n0 + B <= p.end) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int c = 2 * (j + 512 * r);
@@ -66,8 +66,8 @@ __device__ __forceinline__ float fft4_store(const DirectParams &p, const double2
                 const int c = 2 * (j + 512 * r);
                 const float f0 = (float)a[r].x, f1 = (float)(-a[r].y);
                 const int64_t o = off + c;
-                const bool ok0 = c >= cmin && c < cmax && o < oend,
-                           ok1 = c + 1 >= cmin && c + 1 < cmax && o + 1 < oend;
+                const bool ok0 = c >= cmin && c < cmax && o >= 0 && o < oend,
+                           ok1 = c + 1 >= cmin && c + 1 < cmax && o + 1 >= 0 && o + 1 < oend;
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(f0), ys, ok0 ? (int)(o * 4) : (int)0x80000000, 0,
                                                       kNtStore);
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(f1), ys,
@@ -82,7 +82,7 @@ __device__ __forceinline__ float fft4_store(const DirectParams &p, const double2
         for (int r = 0; r < 16; ++r) {
             const int c = 2 * (j + 512 * r);
             const int64_t o = off + c;
-            const bool ok0 = c >= cmin && o < oend, ok1 = c + 1 >= cmin && o + 1 < oend;
+            const bool ok0 = c >= cmin && o >= 0 && o < oend, ok1 = c + 1 >= cmin && o + 1 >= 0 && o + 1 < oend;
             const int oz0 = ok0 ? (int)(o * 8) : (int)0x80000000;
             const int oz1 = ok1 ? (int)(o * 8 + 8) : (int)0x80000000;
             double v0 = a[r].x, v1 = -a[r].y;
@@ -177,7 +177,7 @@ __global__ __launch_bounds__(kFft4NT) void fir_fft4_f64_kernel(DirectParams p, c
         const int c0 = fft_div(u, gd);
 #pragma unroll
         for (int h = 0; h < 2; ++h)
-            fft_load_unit(p, c0, p.start + (int64_t)(u - c0 * gd.nseg) * B, threadIdx.x + kFft4NT * h, v[h]);
+            fft_load_unit(p, c0, p.seg0 + (int64_t)(u - c0 * gd.nseg) * B, threadIdx.x + kFft4NT * h, v[h]);
     }
     __builtin_amdgcn_s_waitcnt(kVmcnt0);
     __syncthreads();
@@ -198,7 +198,7 @@ __global__ __launch_bounds__(kFft4NT) void fir_fft4_f64_kernel(DirectParams p, c
     const int lane = jt & 63;
     const int wv = jt >> 6; // this kernel's wave (0..3); halves h = 0, 1 are 8-wave waves wv, wv + 4
     const int ch = fft_div(u, gd);
-    const int64_t n0 = p.start + (int64_t)(u - ch * gd.nseg) * B;
+    const int64_t n0 = p.seg0 + (int64_t)(u - ch * gd.nseg) * B;
 
     // ---- stage 1, both halves: thread b = jt + 256 h, 16-point DFT over z[512 a + b]
 #pragma unroll
@@ -308,7 +308,7 @@ __global__ __launch_bounds__(kFft4NT) void fir_fft4_f64_kernel(DirectParams p, c
         const int cn = fft_div(un, gd);
 #pragma unroll
         for (int h = 0; h < 2; ++h)
-            fft_load_unit(p, cn, p.start + (int64_t)(un - cn * gd.nseg) * B, jt + kFft4NT * h, v[h]);
+            fft_load_unit(p, cn, p.seg0 + (int64_t)(un - cn * gd.nseg) * B, jt + kFft4NT * h, v[h]);
     }
     wave_lds_sync();
     // ---- stage B': lane (d1, beta0) gathers e1; radix-8 -> gamma0; * W_64^(gamma0 d1)

@@ -404,6 +404,39 @@ int lcfir_ctx_fft_waves(lcfir_ctx *ctx, int32_t *waves) {
     return LCFIR_OK;
 }
 
+// [lo, hi) of lcfir_ctx_window, clipped to [0, n); start < end
+static int range_window(lcfir_ctx *ctx, int64_t n, int64_t start, int64_t end, int64_t &lo, int64_t &hi) {
+    lo = start - ctx->half;
+    hi = end + ctx->half;
+    if (resolve_method(ctx) == LCFIR_METHOD_FFT) {
+        const int rc = ensure_fft(ctx);
+        if (rc) return rc;
+        lcfir::fft_window(ctx->fft, ctx->half, start, end, lo, hi);
+    }
+    lo = std::max<int64_t>(0, lo);
+    hi = std::max(lo, std::min<int64_t>(n, hi));
+    return LCFIR_OK;
+}
+
+int lcfir_ctx_window(lcfir_ctx *ctx, int64_t n, int64_t start, int64_t end, int64_t *lo, int64_t *hi) {
+    if (!ctx || !lo || !hi) return fail(LCFIR_EINVAL, "null argument");
+    if (n < 0 || start < 0 || end < start || end > n)
+        return fail(LCFIR_EINVAL, "bad range [%lld, %lld) for n=%lld", (long long)start, (long long)end,
+                    (long long)n);
+    if (end == start) {
+        *lo = *hi = start;
+        return LCFIR_OK;
+    }
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return fail(LCFIR_EDEVICE, "hipSetDevice(%d) failed", ctx->device);
+    int64_t l = 0, h = 0;
+    const int rc = range_window(ctx, n, start, end, l, h);
+    if (rc) return rc;
+    *lo = l;
+    *hi = h;
+    return LCFIR_OK;
+}
+
 int lcfir_apply_range(lcfir_ctx *ctx, const float *x, int64_t n, float *y, int64_t start,
                       int64_t end, lcfir_progress_fn progress, void *user) {
     if (!ctx || !x || !y) return fail(LCFIR_EINVAL, "null argument");
@@ -411,10 +444,12 @@ int lcfir_apply_range(lcfir_ctx *ctx, const float *x, int64_t n, float *y, int64
         return fail(LCFIR_EINVAL, "bad range [%lld, %lld) for n=%lld", (long long)start,
                     (long long)end, (long long)n);
     if (end == start) return LCFIR_OK;
-    const int64_t lo = std::max<int64_t>(0, start - ctx->half);
-    const int64_t hi = std::min<int64_t>(n, end + ctx->half);
     DeviceGuard g(ctx->device);
     if (!g.ok) return fail(LCFIR_EDEVICE, "hipSetDevice(%d) failed", ctx->device);
+    // the samples the range's units read: every thread's range gives the
+    // whole-channel outputs bit for bit (ProcessFile.cp:60-83 at any -t)
+    int64_t lo = 0, hi = 0;
+    if (const int wrc = range_window(ctx, n, start, end, lo, hi)) return wrc;
     Staging *st = borrow_staging(ctx->device);
     if (!st) return fail(LCFIR_EDEVICE, "stream creation failed");
     int rc = grow(st->d_x, st->x_cap, (size_t)(hi - lo), st->stream);

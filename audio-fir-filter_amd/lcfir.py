@@ -55,6 +55,7 @@ _SIGNATURES = {
     "lcfir_ctx_half": ([_ctxp, ctypes.POINTER(_c_i32)], _c_int),
     "lcfir_ctx_fft_waves": ([_ctxp, ctypes.POINTER(_c_i32)], _c_int),
     "lcfir_ctx_ntaps": ([_ctxp, ctypes.POINTER(_c_i32)], _c_int),
+    "lcfir_ctx_window": ([_ctxp, _c_i64, _c_i64, _c_i64, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i64)], _c_int),
     "lcfir_apply_range": ([_ctxp, _vp, _c_i64, _vp, _c_i64, _c_i64, PROGRESS_FN, _vp], _c_int),
     "lcfir_staging_release": ([_c_int], _c_int),
     "lcfir_staging_count": ([_c_int, ctypes.POINTER(_c_int), ctypes.POINTER(_c_int)], _c_int),
@@ -207,6 +208,14 @@ class Filter:
         n = ctypes.c_int32()
         _check(load().lcfir_ctx_ntaps(self._ctx, ctypes.byref(n)))
         return n.value
+
+    def window(self, n: int, start: int, end: int):
+        """Input window (lo, hi) within [0, n) for which filter_window_dev's
+        outputs [start, end) equal the whole-channel call's bit for bit
+        (lcfir_ctx_window; the FFT method reads whole segments)."""
+        lo, hi = ctypes.c_int64(), ctypes.c_int64()
+        _check(load().lcfir_ctx_window(self._ctx, n, start, end, ctypes.byref(lo), ctypes.byref(hi)))
+        return lo.value, hi.value
 
     @property
     def taps(self) -> np.ndarray:

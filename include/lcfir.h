@@ -82,6 +82,16 @@ int lcfir_ctx_ntaps(const lcfir_ctx *ctx, int32_t *ntaps);
  * LCFIR_FFT_WAVES=4); builds the plan if needed.  0 when the tap count is
  * outside the FFT method's range. */
 int lcfir_ctx_fft_waves(lcfir_ctx *ctx, int32_t *waves);
+/* Input window [*lo, *hi) (within [0, n)) of a channel of n samples that
+ * makes a call for outputs [start, end) reproduce the whole-channel call's
+ * outputs bit for bit, whatever the range: the partition invariance of
+ * FilterCore.h's per-thread ranges (ProcessFile.cp:60-83).  The direct
+ * method needs [start - half, end + half); the FFT method needs the samples
+ * of the whole segments the range touches (its segment grid is anchored at
+ * output 0), a few thousand more.  A narrower window that still covers
+ * [start - half, end + half) gives outputs within 1 f32 ulp of those.
+ * Builds the FFT plan if needed. */
+int lcfir_ctx_window(lcfir_ctx *ctx, int64_t n, int64_t start, int64_t end, int64_t *lo, int64_t *hi);
 
 /* ---- the hot path: host-pointer range call ----------------------------- */
 /* Replaces apply_filter_range(channel, sinc, temp_output, startIdx, endIdx,
@@ -122,7 +132,8 @@ int lcfir_filter_channels_dev(lcfir_ctx *ctx, const float *d_x, int64_t x_stride
  * samples long (channel c's window at d_xw + c*x_stride, element 0 = sample
  * x_lo) and wants outputs [start, end) (channel c's at d_yw + c*y_stride,
  * element 0 = output y_lo).  The window must cover
- * [max(0, start - half), min(n, end + half)).  d_peak (nullable): channel c's
+ * [max(0, start - half), min(n, end + half)); lcfir_ctx_window's window
+ * makes the outputs bit-identical to the whole-channel call's.  d_peak (nullable): channel c's
  * max|y| is max-ed into d_peak[c * peak_stride] (peak_stride 0 folds every
  * channel into one per-file slot, ProcessFile.cp:92-96). */
 int lcfir_filter_window_dev(lcfir_ctx *ctx, const float *d_xw, int64_t x_lo, int64_t x_hi,

@@ -124,6 +124,44 @@ def test_device_batch_runner_fft_pipelined(tt, oracle_mod, ntaps, lanes, normali
     r.close()
 
 
+@pytest.mark.parametrize("ntaps,world", [(4001, 2), (4003, 3), (19201, 4)])
+def test_split_file_ranks_bit_identical(tt, oracle_mod, ntaps, world):
+    """A file split by sample range over `world` ranks (plan_shards, one GPU
+    standing in for all of them): each rank reads lcfir_ctx_window's input
+    window (DeviceBackend.window, the FFT's whole segments), so the ranks'
+    outputs put together equal the unsplit run's bit for bit -- the result
+    does not depend on the GPU count."""
+    torch, lc = tt
+    import batch
+    import synth
+    taps = oracle_mod.design_lowcut(25.0, 48000.0, ntaps)
+    half = (ntaps - 1) // 2
+    n = 250_001
+    x = synth.file_buffer(2, n, 48000.0, file=4, bits=24)
+    flt = lc.Filter(taps, method="fft")
+
+    def run(rank, w):
+        be = batch.DeviceBackend(flt, torch.device("cuda", 0))
+        r = batch.BatchRunner(be, rank, w, [n], 2, half, False, "file",
+                              allreduce_max=lambda t: None)  # the peak exchange is not under test
+        r.prepare(lambda f, lo, hi: x[:, lo:hi])
+        r.step()
+        out = [(sh.start, sh.end, y.cpu().numpy()) for sh, y in r.results()]
+        r.close()
+        return out
+
+    (s0, e0, whole), = run(0, 1)
+    assert (s0, e0) == (0, n)
+    got = np.zeros_like(whole)
+    covered = 0
+    for rank in range(world):
+        for s, e, y in run(rank, world):
+            got[:, s:e] = y
+            covered += e - s
+    assert covered == n
+    assert np.array_equal(got, whole)
+
+
 def _run_batch_checks(torch, oracle_mod, flt, files, taps, normalize, lanes):
     import batch
     be = batch.DeviceBackend(flt, torch.device("cuda", 0), lanes=lanes)

@@ -72,7 +72,13 @@ def test_reference_call_shape(dropin, tmp_path, oracle_mod, threads):
     out = dict(line.split() for line in r.stdout.strip().splitlines())
     assert int(out["progress"]) == x.size  # every sample reported exactly once
     y = np.fromfile(yo, np.float32).reshape(x.shape)
+    import lcfir
+    flt = lcfir.Filter(taps)  # the drop-in's method choice (AUTO)
     for c in range(x.shape[0]):
+        # partition invariance: any thread count gives the one-range bytes
+        whole = np.zeros(x.shape[1], np.float32)
+        flt.apply_range(np.ascontiguousarray(x[c], np.float32), whole, 0, x.shape[1])
+        assert np.array_equal(y[c], whole), (threads, c)
         ref = oracle_mod.filter_channel(x[c], taps, oracle_mod.MODE_LD)
         d = y[c].astype(np.float64) - ref
         assert np.sqrt(np.mean(d * d)) <= 1e-9

@@ -9,7 +9,7 @@ Its outputs are checked against the long-double oracle at
 every edge sample plus random positions, against the default 8-wave kernel
 (<= 1 f32 ulp everywhere), and its windowed calls (odd starts, windows
 shorter than one segment, straddling the range edges) against its own
-whole-channel outputs, bit for bit."""
+whole-channel outputs, bit for bit (input windows from lcfir_ctx_window)."""
 import json
 import os
 import subprocess
@@ -42,8 +42,7 @@ for i, c in enumerate(cases):
     out[f"y{{i}}"] = dy.download((nch, n))
     out[f"pk{{i}}"] = dpk.download(nch)
     for k, (s, e) in enumerate(c["windows"]):
-        half = (len(np.load(c["taps"])) - 1) // 2
-        lo, hi = max(0, s - half), min(n, e + half)
+        lo, hi = flt.window(n, s, e)  # the whole segments: bit for bit
         xw = np.ascontiguousarray(x[:, lo:hi], np.float32)
         dxw = lcfir.DeviceBuffer.from_array(xw); dyw = lcfir.DeviceBuffer(4 * nch * (e - s))
         flt.filter_window_dev(dxw, lo, hi, hi - lo, n, nch, dyw, s, e - s, s, e)

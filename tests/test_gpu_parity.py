@@ -156,6 +156,39 @@ def test_apply_range_dev(lc, oracle_mod, method):
         assert np.array_equal(y, oracle_mod.filter_channel(x, taps, oracle_mod.MODE_FMA))
 
 
+@pytest.mark.parametrize("kind", ["direct", "sym", "general", "parts"])
+def test_partition_invariance(lc, oracle_mod, kind):
+    """SURVEY.md s4's partition invariance (ProcessFile.cp:60-83): the output
+    does not depend on how a channel is split into ranges.  The reference's
+    per-thread chunk hand-off at 1-64 threads (host-pointer ranges, each a
+    concurrent lcfir_apply_range), ragged device ranges (lcfir_apply_range_dev)
+    and the whole-channel launch give the same bytes: the direct method by its
+    fixed FMA order, the FFT by its segment grid anchored at output 0 of the
+    channel (fir_fft.hpp fft_grid_start)."""
+    import synth
+    n = 150_001
+    ntaps = {"direct": 801, "sym": 4001, "general": 4003, "parts": 19201}[kind]
+    taps = oracle_mod.design_lowcut(30.0, 48000.0, ntaps)
+    flt = lc.Filter(taps, method="direct" if kind == "direct" else "fft")
+    x = synth.file_buffer(1, n, 48000.0, file=9, bits=24)
+    y, _ = gpu_filter_channels(lc, flt, x)
+    for threads in (1, 2, 3, 7, 64):
+        assert np.array_equal(lc.filter_channel(x[0], flt, threads), y[0]), threads
+    rng = np.random.default_rng(ntaps)
+    cuts = np.unique(np.r_[0, rng.integers(1, n, 9), 12_384, 12_385, n])
+    dx = lc.DeviceBuffer.from_array(x[0])
+    dy = lc.DeviceBuffer.from_array(np.zeros(n, np.float32))
+    for s_, e_ in zip(cuts[:-1], cuts[1:]):
+        flt.apply_range_dev(dx, n, dy, int(s_), int(e_))
+    lc.sync()
+    assert np.array_equal(dy.download(n), y[0])
+    dx.free()
+    dy.free()
+    idx = _sample_positions(n, ntaps // 2, 1024, 77)
+    ref, _ = oracle_mod.filter_points(x[0], taps, idx, oracle_mod.MODE_LD)
+    assert rms(y[0][idx], ref) <= RMS_TOL and max_ulps(y[0][idx], ref) <= 1
+
+
 def test_concurrent_contexts_and_threads(lc, oracle_mod):
     """Several filters used from several threads at once (re-entrancy)."""
     g1, g2 = load_golden("random_int24"), load_golden("sine")
@@ -331,8 +364,22 @@ def test_fft_partitioned_long_filters(lc, oracle_mod, ntaps):
     # range): every partition's shifted reads must stay inside that window
     half = (ntaps - 1) // 2
     for start, end in [(12_345, n - 23_456), (half + 7, half + 70_007), (n - 5_000, n)]:
-        yw = gpu_filter_window(lc, flt, x, start, end, max(0, start - half), min(n, end + half))
-        assert np.array_equal(yw, y[:, start:end]), (start, end)
+        check_window(lc, flt, x, y, start, end)
+
+
+def check_window(lc, flt, x, y, start, end):
+    """Outputs [start, end) of a windowed call against the whole-channel
+    outputs y: bit for bit from lcfir_ctx_window's window (the FFT's whole
+    segments), within 1 f32 ulp from the narrowest window the outputs need
+    (its edge segments read zeros where the whole channel has samples)."""
+    n = x.shape[1]
+    half = (flt.ntaps - 1) // 2
+    lo, hi = flt.window(n, start, end)
+    assert lo <= max(0, start - half) and hi >= min(n, end + half)
+    yw = gpu_filter_window(lc, flt, x, start, end, lo, hi)
+    assert np.array_equal(yw, y[:, start:end]), (start, end, lo, hi)
+    yn = gpu_filter_window(lc, flt, x, start, end, max(0, start - half), min(n, end + half))
+    assert max_ulps(yn, y[:, start:end]) <= 1 and rms(yn, y[:, start:end]) <= RMS_TOL, (start, end)
 
 
 def gpu_filter_window(lc, flt, x, start, end, x_lo, x_hi):
@@ -365,7 +412,7 @@ np.savez({out!r}, y=dy.download((1, {n})), pk=dpk.download(1))
 """
 
 
-def test_fft_partitioned_chunk_seams(oracle_mod, tmp_path):
+def test_fft_partitioned_chunk_seams(lc, oracle_mod, tmp_path):
     """A partitioned filter with launches split into 65 536-output chunks
     (LCFIR_FFT_CHUNK, read once per process, so in a child process): the f64
     partial-sum scratch restarts at every seam.  Checked around each seam."""
@@ -387,6 +434,10 @@ def test_fft_partitioned_chunk_seams(oracle_mod, tmp_path):
     y, pk = d["y"][0], d["pk"][0]
     import synth
     x = synth.file_buffer(1, n, 48000.0, file=6, bits=24)[0]
+    # chunks are whole segments of the channel's grid: the unchunked launch
+    # (this process) gives the same bytes
+    y_one, pk_one = gpu_filter_channels(lc, lc.Filter(taps, method="fft"), x[None, :])
+    assert np.array_equal(y, y_one[0]) and pk == pk_one[0]
     seams = np.r_[[s + o for s in range(chunk, n, chunk) for o in range(-3, 3)]]
     idx = np.unique(np.r_[_sample_positions(n, 9600, 512, 61), seams])
     ref_ld, _ = oracle_mod.filter_points(x, taps, idx, oracle_mod.MODE_LD)
@@ -488,8 +539,7 @@ def test_fft_zero_phase_form(lc, oracle_mod, tmp_path, ntaps, perturb):
         assert rms(y[c][idx], ref_ld) <= RMS_TOL
         assert max_ulps(y[c][idx], ref_ld) <= 1
     for start, end in [(1, n - 1), (half - 1, half + 12_385), (77_777, 77_778), (n - 13_000, n)]:
-        yw = gpu_filter_window(lc, flt, x, start, end, max(0, start - half), min(n, end + half))
-        assert np.array_equal(yw, y[:, start:end]), (start, end)
+        check_window(lc, flt, x, y, start, end)
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     np.save(tmp_path / "taps.npy", taps)
     code = _SYM_CHILD.format(pkg=os.path.join(root, "audio-fir-filter_amd"), oracle=os.path.join(root, "oracle"),
