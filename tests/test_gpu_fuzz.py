@@ -11,7 +11,9 @@ both methods.  Every case against the oracle at sampled positions:
     the narrowest window [start - half, end + half): bit for bit for the
     direct method, within 1 f32 ulp for the FFT (whose edge segments then
     read zeros where the whole channel has samples);
-  * the fused per-channel peak equal to max |y| of the whole channel.
+  * the fused per-channel peak equal to max |y| of the whole channel;
+  * channel 0 as ragged device ranges equal to the whole-channel call, bit
+    for bit (partition invariance).
 
 A second set fuzzes lcfir_filter_window_norm_dev (a previous file's normalize
 carried by the filter call) against the separate filter + normalize calls.
@@ -97,6 +99,19 @@ def test_random_case(oracle_mod, seed):
             ref_fma, _ = oracle_mod.filter_points(x[c], taps, idx, oracle_mod.MODE_FMA)
             assert np.array_equal(y[c][idx], ref_fma), (seed, c)
         assert pk[c] == np.abs(y[c]).max(), (seed, c)
+
+    # partition invariance: channel 0 as ragged device ranges (each call reads
+    # the whole channel) gives the whole-channel bytes
+    cuts = np.unique(np.r_[0, rng.integers(0, n + 1, int(rng.integers(1, 6))), n])
+    dx0 = lc.DeviceBuffer.from_array(np.ascontiguousarray(x[0]))
+    dy0 = lc.DeviceBuffer.from_array(np.zeros(n, np.float32))
+    for s_, e_ in zip(cuts[:-1], cuts[1:]):
+        flt.apply_range_dev(dx0, n, dy0, int(s_), int(e_))
+    lc.sync()
+    y0 = dy0.download(n)
+    dx0.free()
+    dy0.free()
+    assert np.array_equal(y0, y[0]), (seed, cuts.tolist())
 
     # sub-ranges from only their input window (a file sharded by sample range)
     for _ in range(3):
