@@ -79,6 +79,8 @@ def parse():
                          "the exclusive kernel time roofline.kernel_ms is measured on")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--no-ingest", action="store_true",
+                    help="skip the PCIe ingest probe (pinned PCM bytes -> HBM + on-device decode)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     a = ap.parse_args()
@@ -140,6 +142,50 @@ def cpu_baseline(x0, taps, budget_s, max_cores=16):
             "sample": f"first {n} samples of file 0 (channels laid end to end), {taps.size} "
                       f"taps, oracle ORACLE_FMA three-loop restatement, {cores} pthreads, "
                       f"{dt:.1f} s"}
+
+
+def ingest_probe(torch, lcfir, x, bits, dev, reps=5, max_frames=28_800_000):
+    """What the resident-input `value` leaves out (PCIe H2D
+    reported separately): one file's samples as interleaved PCM bytes in
+    pinned host memory, copied to HBM and decoded to planar f32 on the device
+    (lcfir_decode_pcm_dev) -- the lowcut tool's ingest.  Up to max_frames
+    frames of x ([nch][frames] f32), HIP events on a side stream, median of
+    reps; the decoded samples are checked against x."""
+    import numpy as np
+    nch, frames = x.shape
+    frames = min(frames, max_frames)
+    fmt = {16: "s16le", 24: "s24le"}.get(bits or 0, "f32le")
+    xi = np.ascontiguousarray(x[:, :frames].T)  # interleaved [frames][nch]
+    if fmt == "f32le":
+        pcm = xi.astype("<f4").view(np.uint8).reshape(-1)
+    else:
+        v = np.rint(xi.astype(np.float64) * 2.0 ** (bits - 1)).astype("<i4")
+        pcm = np.ascontiguousarray(v.view(np.uint8).reshape(-1, 4)[:, :bits // 8]).reshape(-1)
+    host = torch.empty(pcm.size, dtype=torch.uint8, pin_memory=True)
+    host.numpy()[:] = pcm
+    d_pcm = torch.empty(pcm.size, dtype=torch.uint8, device=dev)
+    d_out = torch.empty((nch, frames), dtype=torch.float32, device=dev)
+    s = torch.cuda.Stream(dev)
+    h2d, dec = [], []
+    with torch.cuda.stream(s):
+        for _ in range(reps + 1):
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            e[0].record(s)
+            d_pcm.copy_(host, non_blocking=True)
+            e[1].record(s)
+            lcfir.decode_pcm_dev(d_pcm, fmt, nch, frames, d_out, frames, stream=s.cuda_stream)
+            e[2].record(s)
+            s.synchronize()
+            h2d.append(e[0].elapsed_time(e[1]))
+            dec.append(e[1].elapsed_time(e[2]))
+    h2d, dec = sorted(h2d[1:])[reps // 2], sorted(dec[1:])[reps // 2]
+    ok = bool(torch.equal(d_out.cpu(), torch.from_numpy(np.ascontiguousarray(x[:, :frames]))))
+    return {"format": fmt, "frames": frames, "channels": nch, "bytes": int(pcm.size),
+            "h2d_ms": round(h2d, 4), "h2d_GBps": round(pcm.size / h2d / 1e6, 2),
+            "decode_ms": round(dec, 4), "decode_exact": ok,
+            "msamples_per_s": round(nch * frames / (h2d + dec) / 1e3, 1),
+            "note": "pinned interleaved PCM -> HBM -> planar f32 on one stream, median of "
+                    f"{reps}; outside the timed region and never `value`"}
 
 
 def parity_probe(x, y, taps, start, gain=None, k=512):
@@ -341,6 +387,10 @@ def main():
         sh0, y0 = runner.results()[0]
         probe = (sh0, y0.cpu().numpy(), float(runner.peaks[sh0.file].item()))
 
+    ingest = None
+    if not args.no_ingest and runner.shards:
+        ingest = ingest_probe(torch, lcfir, file_samples(runner.shards[0].file), bits, dev)
+
     total_samples = torch.tensor([float(my_samples)], dtype=torch.float64, device=dev)
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
@@ -441,6 +491,8 @@ def main():
                        "tol": 1e-9, "of": "outputs of the last timed step (rank 0, first shard)"},
             "preroll": {"seconds": round(preroll_s, 3), "steps": preroll_steps},
         }
+        if ingest is not None:
+            line["ingest"] = ingest  # rank 0's
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(file_samples(0).reshape(-1), taps,
                                                 args.cpu_seconds,

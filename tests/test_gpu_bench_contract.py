@@ -44,3 +44,6 @@ def test_bench_json_line(lanes):
     assert cb["value"] > 0 and cb["kind"] == "port" and cb["cores"] >= 1 and cb["sample"]
     assert d["parity"]["rms_vs_longdouble"] <= d["parity"]["tol"] == 1e-9
     assert d["parity"]["max_ulp"] <= 1.0
+    ing = d["ingest"]  # PCIe ingest probe: reported beside `value`, never in it
+    assert ing["format"] == "s24le" and ing["decode_exact"] is True
+    assert ing["bytes"] == 3 * ing["frames"] * ing["channels"] and 0 < ing["h2d_GBps"] < 200
