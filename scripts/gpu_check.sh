@@ -23,7 +23,7 @@ step pytest_gpu 1200 python -u -m pytest tests -m gpu -x -v --timeout 300 --time
 step bench 600 python bench.py "$@"
 cd /tmp && export TMPDIR=/tmp
 step rocprof 600 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof_$TAG" -o bench -- \
-    python3 "$ROOT/bench.py" --no-cpu-baseline --no-parity "$@"
+    python3 "$ROOT/bench.py" --no-cpu-baseline --no-parity --no-ingest "$@"
 cp "$OUT/prof_$TAG/bench_kernel_stats.csv" "$OUT/kernel_stats_$TAG.csv"
 python3 "$ROOT/scripts/trace_exclusive.py" "$OUT/prof_$TAG/bench_kernel_trace.csv" > "$OUT/exclusive_from_trace_$TAG.json"
 i=0
@@ -31,7 +31,7 @@ for c in FETCH_SIZE WRITE_SIZE "SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VAL
     i=$((i+1))
     step "pmc_$i" 600 rocprofv3 --pmc $c --kernel-include-regex 'fir_' -f csv \
         -d "$OUT/pmc_$TAG/p_$i" -o pmc -- \
-        python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-parity "$@"
+        python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-parity --no-ingest "$@"
 done
 cd "$ROOT"
 python scripts/pmc_summary.py "$OUT/pmc_$TAG" --json "$OUT/pmc_summary_$TAG.json" > /dev/null
