@@ -275,11 +275,14 @@ class DeviceBackend(Backend):
     """gfx950 kernels through the C ABI on torch-allocated HBM: lane 0 is the
     caller's current stream, lanes 1.. are streams of their own."""
 
-    def __init__(self, flt, device, lanes: int = 1):
+    def __init__(self, flt, device, lanes: int = 1, own_streams: bool = False):
         import torch
         import lcfir
         self.torch, self.lc, self.flt, self.dev = torch, lcfir, flt, device
-        self.streams = [torch.cuda.current_stream(device)]
+        # own_streams: lane 0 too gets a stream of its own (HIP graph capture
+        # cannot run on the default stream; GraphedSteps); it is the current
+        # stream after every step
+        self.streams = [torch.cuda.Stream(device) if own_streams else torch.cuda.current_stream(device)]
         self.streams += [torch.cuda.Stream(device) for _ in range(lanes - 1)]
         self.stream = self.streams[0]
         self.sp = self.stream.cuda_stream
@@ -347,6 +350,41 @@ class DeviceBackend(Backend):
         p = peaks if slot is None else peaks[slot:slot + 1]
         self.lc.normalize_clear_dev(yw, yw.shape[1], nch, count, p, p.numel(), force, clear,
                                     clear.numel(), self.sp)
+
+
+class GraphedSteps:
+    """BatchRunner steps replayed from one captured HIP graph, for launch-bound
+    batches (config 1: 48 000 samples, three launches of a few microseconds
+    per step, where host-side issue sets the rate).  The graph holds two
+    rounds of steps over every lane (2 x lanes steps), so each lane's peak
+    vectors alternate exactly as in eager steps and a replay leaves the
+    runner's buffers as the eager steps would: replay() == 2 x lanes step()s.
+    Lanes fork from and join back to lane 0's stream inside the capture, so
+    the lanes' steps run concurrently on the device.  Needs a DeviceBackend
+    with own_streams=True and no collective in the step."""
+
+    def __init__(self, runner, backend):
+        torch = backend.torch
+        if runner.exchange:
+            raise ValueError("a step with a peak exchange (collective) is not captured")
+        s0 = backend.streams[0]
+        if s0 == torch.cuda.default_stream(backend.dev):
+            raise ValueError("lane 0 must be a stream of its own: DeviceBackend(own_streams=True)")
+        self.runner, self.backend = runner, backend
+        self.per_replay = 2 * runner.lanes
+        torch.cuda.synchronize(backend.dev)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph, stream=s0):
+            for s in backend.streams[1:]:
+                s.wait_stream(s0)
+            for _ in range(self.per_replay):
+                runner.step()
+            for s in backend.streams[1:]:
+                s0.wait_stream(s)
+
+    def replay(self):
+        """Run per_replay steps (on lane 0's stream; the caller syncs)."""
+        self.graph.replay()
 
 
 def torch_allreduce_max(group=None):

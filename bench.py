@@ -79,6 +79,10 @@ def parse():
                          "the exclusive kernel time roofline.kernel_ms is measured on")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
+                    help="replay the steps from a captured HIP graph (batch.GraphedSteps: 2 x lanes "
+                         "steps per replay); auto = on for config 1, whose 48 000-sample steps are "
+                         "bound by host-side launch issue")
     ap.add_argument("--no-ingest", action="store_true",
                     help="skip the PCIe ingest probe (pinned PCM bytes -> HBM + on-device decode)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
@@ -96,8 +100,10 @@ def parse():
         a.files = 8 if a.files is None else a.files
         a.seconds = 3600.0 if a.seconds is None else a.seconds
         a.normalize = a.normalize or a.config == 5
+    if a.graph == "auto":
+        a.graph = "on" if a.config == 1 else "off"
     if a.lanes is None:
-        a.lanes = 2 if a.config in (1, 2, 3) else 1
+        a.lanes = (10 if a.graph == "on" else 2) if a.config in (1, 2, 3) else 1
     return a
 
 
@@ -309,7 +315,8 @@ def main():
     flt = lcfir.Filter(taps, device=local, method=args.method)
     method = flt.method
 
-    backend = TimedBackend(batch.DeviceBackend(flt, dev, lanes=args.lanes), torch)
+    backend = TimedBackend(batch.DeviceBackend(flt, dev, lanes=args.lanes, own_streams=args.graph == "on"),
+                           torch)
     runner = batch.BatchRunner(backend, rank, world, [n] * nfiles, nch, half, args.normalize,
                                args.peak_scope, batch.torch_allreduce_max(), lanes=args.lanes,
                                fuse_normalize=not args.no_fuse_normalize)
@@ -363,13 +370,22 @@ def main():
     backend.events = []
     for _ in range(args.warmup):
         runner.step()
+    graphed = None
+    if args.graph == "on" and not runner.exchange:
+        # captured after the eager warmup (plans, scratch and kernel
+        # attributes exist by now); replays run the same steps
+        graphed = batch.GraphedSteps(runner, backend.inner)
+        graphed.replay()  # untimed: the first replay uploads the graph
+    n_replay, n_eager = divmod(args.steps, graphed.per_replay) if graphed else (0, args.steps)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     backend.record = True
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(n_replay):
+        graphed.replay()
+    for _ in range(n_eager):
         runner.step()
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -462,6 +478,8 @@ def main():
                 "peak_exchange": runner.exchange,
                 "fused_normalize": runner.fuse and len(runner.shards) > 1,
                 "lanes": args.lanes,
+                "hip_graph": {"replays": n_replay, "steps_per_replay": graphed.per_replay,
+                              "eager_steps": n_eager} if graphed else None,
             },
             "roofline": {
                 "bound": "hbm",

@@ -162,6 +162,59 @@ def test_split_file_ranks_bit_identical(tt, oracle_mod, ntaps, world):
     assert np.array_equal(got, whole)
 
 
+@pytest.mark.parametrize("lanes,normalize", [(1, False), (3, True)])
+def test_graphed_steps_equal_eager(tt, oracle_mod, lanes, normalize):
+    """batch.GraphedSteps (the steps captured into one HIP graph, 2 x lanes
+    steps per replay, lanes forked from lane 0's stream) gives the eager
+    steps' bytes: config 1's kernel (19 201 taps, two partitions, its
+    partial-sum scratch) over two 48 000-sample files, one loud.  The output
+    buffers are poisoned before the replay, so they come from the graph."""
+    torch, lc = tt
+    import batch
+    import synth
+    taps = oracle_mod.design_lowcut(20.0, 48000.0, 19201)
+    half = (taps.size - 1) // 2
+    files = [synth.file_buffer(1, 48_000, 48000.0, file=f, bits=16) for f in range(2)]
+    files[1] = (files[1] * np.float32(2.0)).astype(np.float32)
+    flt = lc.Filter(taps, method="fft")
+    dev = torch.device("cuda", 0)
+
+    def runner():
+        be = batch.DeviceBackend(flt, dev, lanes=lanes, own_streams=True)
+        r = batch.BatchRunner(be, 0, 1, [48_000, 48_000], 1, half, normalize, "file", lanes=lanes)
+        r.prepare(lambda f, lo, hi: files[f][:, lo:hi])
+        for _ in range(2 * lanes):
+            r.step()
+        return be, r
+
+    be, r = runner()
+    want = [(sh.file, y.cpu().numpy()) for sh, y in r.results()]
+    want_pk = r.peaks.cpu().numpy()
+    r.close()
+    be, r = runner()
+    g = batch.GraphedSteps(r, be)
+    assert g.per_replay == 2 * lanes
+    for outs in r._outs:
+        for y in outs:
+            y.fill_(float("nan"))
+    g.replay()
+    got = [(sh.file, y.cpu().numpy()) for sh, y in r.results()]
+    assert np.array_equal(r.peaks.cpu().numpy(), want_pk)
+    for (fa, ya), (fb, yb) in zip(want, got):
+        assert fa == fb and np.array_equal(ya, yb), fa
+    g.replay()  # again: the same bytes (each lane's peak vectors alternate inside the graph)
+    assert all(np.array_equal(y.cpu().numpy(), w) for (_, y), (_, w) in zip(r.results(), want))
+    r.close()
+    for f, y in want:
+        ref = files[f].copy()
+        oracle_mod.process_buffer(ref, taps, nthreads=1, normalize=normalize, mode=oracle_mod.MODE_LD)
+        assert _ulps(y, ref).max() <= 1, f
+    torch.cuda.set_stream(torch.cuda.default_stream(dev))  # the steps left lane 0's stream current
+    be = batch.DeviceBackend(flt, dev)  # lane 0 = the default stream: not capturable
+    with pytest.raises(ValueError):
+        batch.GraphedSteps(batch.BatchRunner(be, 0, 1, [48_000], 1, half), be)
+
+
 def _run_batch_checks(torch, oracle_mod, flt, files, taps, normalize, lanes):
     import batch
     be = batch.DeviceBackend(flt, torch.device("cuda", 0), lanes=lanes)
