@@ -353,38 +353,60 @@ class DeviceBackend(Backend):
 
 
 class GraphedSteps:
-    """BatchRunner steps replayed from one captured HIP graph, for launch-bound
+    """BatchRunner steps replayed from captured HIP graphs, for launch-bound
     batches (config 1: 48 000 samples, three launches of a few microseconds
-    per step, where host-side issue sets the rate).  The graph holds two
-    rounds of steps over every lane (2 x lanes steps), so each lane's peak
-    vectors alternate exactly as in eager steps and a replay leaves the
-    runner's buffers as the eager steps would: replay() == 2 x lanes step()s.
-    Lanes fork from and join back to lane 0's stream inside the capture, so
-    the lanes' steps run concurrently on the device.  Needs a DeviceBackend
-    with own_streams=True and no collective in the step."""
+    per step, where host-side issue sets the rate).  Each lane's two next
+    steps are captured on that lane's stream, so the lane's peak vectors
+    alternate exactly as in eager steps and a replay leaves the runner's
+    buffers as the eager steps would: replay() == 2 x lanes step()s (the
+    lanes' steps touch disjoint buffers, so their order across lanes does not
+    change a byte).  per_lane=False (default) captures all of them into one
+    graph, the lanes forked from lane 0's stream; per_lane=True keeps one
+    graph per lane, replayed on the lanes' own streams (config 1: 2.53 against
+    3.24 Gs/s for one graph at 10 lanes -- each graph launch costs host time).
+    Needs a DeviceBackend with own_streams=True and no collective in the step."""
 
-    def __init__(self, runner, backend):
+    def __init__(self, runner, backend, per_lane: bool = False):
         torch = backend.torch
         if runner.exchange:
             raise ValueError("a step with a peak exchange (collective) is not captured")
         s0 = backend.streams[0]
         if s0 == torch.cuda.default_stream(backend.dev):
             raise ValueError("lane 0 must be a stream of its own: DeviceBackend(own_streams=True)")
+        while runner._lane != 0:  # eager steps up to a round boundary: the capture starts on lane 0
+            runner.step()
         self.runner, self.backend = runner, backend
         self.per_replay = 2 * runner.lanes
         torch.cuda.synchronize(backend.dev)
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph, stream=s0):
-            for s in backend.streams[1:]:
-                s.wait_stream(s0)
-            for _ in range(self.per_replay):
-                runner.step()
-            for s in backend.streams[1:]:
-                s0.wait_stream(s)
+        self.graphs = []
+        if per_lane:
+            for lane, s in enumerate(backend.streams):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=s):
+                    for _ in range(2):
+                        runner._lane = lane
+                        runner.step()
+                    torch.cuda.set_stream(s)  # step() ends on lane 0; the capture ends on s
+                self.graphs.append((s, g))
+            runner._lane = 0  # as after 2 x lanes eager steps from lane 0
+        else:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s0):
+                for s in backend.streams[1:]:
+                    s.wait_stream(s0)
+                for _ in range(self.per_replay):
+                    runner.step()
+                for s in backend.streams[1:]:
+                    s0.wait_stream(s)
+            self.graphs.append((s0, g))
+        runner._last = runner.lanes - 1
 
     def replay(self):
-        """Run per_replay steps (on lane 0's stream; the caller syncs)."""
-        self.graph.replay()
+        """Run per_replay steps, each graph on its lane's stream (the caller syncs)."""
+        torch = self.backend.torch
+        for s, g in self.graphs:
+            with torch.cuda.stream(s):
+                g.replay()
 
 
 def torch_allreduce_max(group=None):

@@ -83,6 +83,9 @@ def parse():
                     help="replay the steps from a captured HIP graph (batch.GraphedSteps: 2 x lanes "
                          "steps per replay); auto = on for config 1, whose 48 000-sample steps are "
                          "bound by host-side launch issue")
+    ap.add_argument("--graph-per-lane", action="store_true",
+                    help="one graph per lane replayed on its own stream instead of one graph for all "
+                         "lanes (GraphedSteps(per_lane=True); measured slower for config 1)")
     ap.add_argument("--no-ingest", action="store_true",
                     help="skip the PCIe ingest probe (pinned PCM bytes -> HBM + on-device decode)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
@@ -374,7 +377,7 @@ def main():
     if args.graph == "on" and not runner.exchange:
         # captured after the eager warmup (plans, scratch and kernel
         # attributes exist by now); replays run the same steps
-        graphed = batch.GraphedSteps(runner, backend.inner)
+        graphed = batch.GraphedSteps(runner, backend.inner, per_lane=args.graph_per_lane)
         graphed.replay()  # untimed: the first replay uploads the graph
     n_replay, n_eager = divmod(args.steps, graphed.per_replay) if graphed else (0, args.steps)
     torch.cuda.synchronize(dev)
@@ -479,7 +482,7 @@ def main():
                 "fused_normalize": runner.fuse and len(runner.shards) > 1,
                 "lanes": args.lanes,
                 "hip_graph": {"replays": n_replay, "steps_per_replay": graphed.per_replay,
-                              "eager_steps": n_eager} if graphed else None,
+                              "graphs": len(graphed.graphs), "eager_steps": n_eager} if graphed else None,
             },
             "roofline": {
                 "bound": "hbm",

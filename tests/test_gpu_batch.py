@@ -162,8 +162,8 @@ def test_split_file_ranks_bit_identical(tt, oracle_mod, ntaps, world):
     assert np.array_equal(got, whole)
 
 
-@pytest.mark.parametrize("lanes,normalize", [(1, False), (3, True)])
-def test_graphed_steps_equal_eager(tt, oracle_mod, lanes, normalize):
+@pytest.mark.parametrize("lanes,normalize,per_lane", [(1, False, True), (3, True, True), (3, True, False)])
+def test_graphed_steps_equal_eager(tt, oracle_mod, lanes, normalize, per_lane):
     """batch.GraphedSteps (the steps captured into one HIP graph, 2 x lanes
     steps per replay, lanes forked from lane 0's stream) gives the eager
     steps' bytes: config 1's kernel (19 201 taps, two partitions, its
@@ -192,17 +192,19 @@ def test_graphed_steps_equal_eager(tt, oracle_mod, lanes, normalize):
     want_pk = r.peaks.cpu().numpy()
     r.close()
     be, r = runner()
-    g = batch.GraphedSteps(r, be)
-    assert g.per_replay == 2 * lanes
+    g = batch.GraphedSteps(r, be, per_lane=per_lane)
+    assert g.per_replay == 2 * lanes and len(g.graphs) == (lanes if per_lane else 1)
     for outs in r._outs:
         for y in outs:
             y.fill_(float("nan"))
     g.replay()
+    torch.cuda.synchronize(dev)
     got = [(sh.file, y.cpu().numpy()) for sh, y in r.results()]
     assert np.array_equal(r.peaks.cpu().numpy(), want_pk)
     for (fa, ya), (fb, yb) in zip(want, got):
         assert fa == fb and np.array_equal(ya, yb), fa
     g.replay()  # again: the same bytes (each lane's peak vectors alternate inside the graph)
+    torch.cuda.synchronize(dev)
     assert all(np.array_equal(y.cpu().numpy(), w) for (_, y), (_, w) in zip(r.results(), want))
     r.close()
     for f, y in want:
