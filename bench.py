@@ -496,7 +496,8 @@ def main():
                 "kernel_ms_note": f"exclusive: {kern_launches} launches of the filter alone on one "
                                   f"stream right after the pre-roll (HIP events on that stream)",
                 "launches_timed": kern_launches,
-                "overlapped_kernel_ms": round(overlapped_ms, 6),
+                # None when the timed steps were graph replays (no per-launch events)
+                "overlapped_kernel_ms": round(overlapped_ms, 6) if launches else None,
                 "bytes_per_unit": 4,
                 "binding": "fp64-valu",
                 "direct_equiv_fp64_tflops": round(direct_tflops, 3),
