@@ -219,3 +219,68 @@ def test_batch_duplicate_destination(tmp_path):
     solo = tmp_path / "solo.wav"
     lowcut("-f", 20, "-s", 48, xs[1], solo)
     assert open(outdir / "x.wav", "rb").read() == open(solo, "rb").read() != first
+
+
+def _random_file(rng, tmp_path, i):
+    rate = int(rng.choice([22050, 44100, 48000, 96000]))
+    nch = int(rng.integers(1, 7))
+    n = int(rng.choice([1, 7, 100, 5000, 30001]))
+    kind = str(rng.choice(["wav", "wavx", "aif", "aifc"]))
+    if kind.startswith("wav"):
+        fmt, comp = str(rng.choice(["s16le", "s24le", "s32le", "f32le"])), None
+    elif kind == "aif":
+        fmt, comp = str(rng.choice(["s16be", "s24be", "s32be"])), None
+    else:
+        fmt, comp = [("s16le", b"sowt"), ("f32be", b"fl32"), ("s24be", b"NONE")][int(rng.integers(3))]
+    amp = float(rng.choice([0.3, 0.9]))
+    x = tone(nch, n, rate, amp=amp)
+    if fmt.startswith("f32") and rng.random() < 0.5:
+        x = (x * np.float32(3.0)).astype(np.float32)  # float source above full scale: the >1 rule
+    extra = [(b"LIST", b"INFOICMT" + bytes([int(rng.integers(1, 9))]) + b"\x00\x00\x00odd")] \
+        if rng.random() < 0.5 else []
+    p = tmp_path / f"r{i}.{'wav' if kind.startswith('wav') else 'aif'}"
+    if kind.startswith("wav"):
+        pcm_ref.write_wave(p, x, rate, fmt, extensible=kind == "wavx", extra_chunks=extra)
+    else:
+        pcm_ref.write_aiff(p, x, rate, fmt, aifc_comp=comp, extra_chunks=extra)
+    return p, x, rate, fmt
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("LCFIR_CLI_SEED0", "0")),
+                                  int(os.environ.get("LCFIR_CLI_SEED0", "0"))
+                                  + int(os.environ.get("LCFIR_CLI_SEEDS", "3"))))
+def test_cli_random_batch(tmp_path, oracle_mod, seed):
+    """Seeded batches of six random files through the tool's pipeline:
+    WAVE / WAVE_FORMAT_EXTENSIBLE / AIFF / AIFF-C, 16/24/32-bit and float
+    samples, 1-6 channels, 1 .. 30 001 frames (shorter than the filter
+    included), four rates, odd-length extra chunks, random -f / -s / -n.
+    Every output against the oracle's process_file (check_file); at most a
+    couple of 1-LSB quantiser-boundary differences per file."""
+    rng = np.random.default_rng(700 + seed)
+    freq, slope = float(rng.uniform(10, 200)), float(rng.uniform(30, 200))
+    normalize = bool(rng.random() < 0.5)
+    srcs = [_random_file(rng, tmp_path, i) for i in range(6)]
+    outdir = tmp_path / "out"
+    lowcut(*(["-n"] if normalize else []), "-f", f"{freq:.3f}", "-s", f"{slope:.3f}",
+           *[s[0] for s in srcs], outdir)
+    for p, x, rate, fmt in srcs:
+        a, b = open(p, "rb").read(), open(outdir / p.name, "rb").read()
+        d = info(p)
+        off, nbytes = int(d["data_offset"]), int(d["data_bytes"])
+        assert len(a) == len(b) and a[:off] == b[:off] and a[off + nbytes:] == b[off + nbytes:], p.name
+        nch = x.shape[0]
+        xq = pcm_ref.np_decode(pcm_ref.np_encode(x, fmt), fmt, nch)
+        got = pcm_ref.np_decode(b[off:off + nbytes], fmt, nch)
+        want_f = expected(oracle_mod, xq, rate, fmt, float(f"{freq:.3f}"), float(f"{slope:.3f}"), normalize)
+        if fmt.startswith("f32"):
+            dd = got.astype(np.float64) - want_f
+            assert np.sqrt(np.mean(dd * dd)) <= 1e-9, p.name
+            assert np.abs(got).max() <= 1.0 or not normalize, p.name
+        else:
+            want = pcm_ref.np_decode(pcm_ref.np_encode(want_f, fmt), fmt, nch)
+            lsb = 1.0 / (1 << (8 * pcm_ref.NB[fmt[:3]] - 1))
+            diff = np.abs(got.astype(np.float64) - want.astype(np.float64))
+            # one quantiser step, or (32-bit samples, finer than f32) one f32 ulp of the filter output
+            tol = lsb * 1.000001 + np.spacing(np.abs(want_f).astype(np.float32)).astype(np.float64)
+            assert np.all(diff <= tol), p.name
+            assert np.sum(diff > 0) <= max(2, 1e-4 * diff.size), p.name
