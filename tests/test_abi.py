@@ -55,6 +55,8 @@ def test_null_arguments_rejected():
     assert lib.lcfir_filter_channels_dev(None, None, 0, 1, 1, None, 0, None, None) == lcfir.EINVAL
     assert lib.lcfir_peak_dev(None, 0, 1, 1, None, None) == lcfir.EINVAL
     assert lib.lcfir_normalize_dev(None, 0, 1, 1, None, 1, 0, None) == lcfir.EINVAL
+    lo, hi = ctypes.c_int64(), ctypes.c_int64()
+    assert lib.lcfir_ctx_window(None, 10, 0, 10, ctypes.byref(lo), ctypes.byref(hi)) == lcfir.EINVAL
     assert lib.lcfir_ctx_destroy(None) == lcfir.OK
 
 
