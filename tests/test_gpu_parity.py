@@ -189,6 +189,39 @@ def test_partition_invariance(lc, oracle_mod, kind):
     assert rms(y[0][idx], ref) <= RMS_TOL and max_ulps(y[0][idx], ref) <= 1
 
 
+@pytest.mark.parametrize("ntaps", [4001, 4003, 19201])
+def test_adversarial_inputs(lc, oracle_mod, ntaps):
+    """Full-scale inputs that stress the FFT's dynamic range, against the
+    long-double oracle at every edge sample plus random positions (RMS <= 1e-9,
+    <= 1 f32 ulp with the 1e-12 floor for outputs that cancel to ~0):
+    Nyquist (+-1 alternating: passes the low-cut at full gain), full-scale DC
+    (cancels to ~0 in the interior), the sign-matched input that drives one
+    output to sum|h| (the largest any +-1 input can reach), a full-scale square
+    wave at the cutoff, and isolated full-scale impulses at both edges."""
+    n = 60_001
+    taps = oracle_mod.design_lowcut(20.0, 48000.0, ntaps)
+    half = (ntaps - 1) // 2
+    k = np.arange(n)
+    matched = np.ones(n)
+    n0 = n // 2
+    matched[n0 - half:n0 - half + ntaps] = np.where(taps >= 0, 1.0, -1.0)
+    square = np.where((k // 1200) % 2 == 0, 1.0, -1.0)  # 20 Hz at 48 kHz
+    edges = np.zeros(n)
+    edges[[0, 1, n - 2, n - 1]] = [1.0, -1.0, -1.0, 1.0]
+    x = np.stack([(-1.0) ** k, np.full(n, 1.0 - 2.0 ** -23), matched, square, edges]).astype(np.float32)
+    flt = lc.Filter(taps, method="fft")
+    y, pk = gpu_filter_channels(lc, flt, x)
+    for c in range(x.shape[0]):
+        idx = _sample_positions(n, half, 1024, 40 + c)
+        if c == 2:
+            idx = np.unique(np.r_[idx, n0 - 2:n0 + 3])
+        ref, _ = oracle_mod.filter_points(x[c], taps, idx, oracle_mod.MODE_LD)
+        assert rms(y[c][idx], ref) <= RMS_TOL, c
+        assert max_ulps(y[c][idx], ref) <= 1, c
+        assert pk[c] == np.abs(y[c]).max(), c
+    assert abs(float(y[2][n0]) - float(np.abs(taps).sum())) <= 1e-6 * float(np.abs(taps).sum())
+
+
 def test_concurrent_contexts_and_threads(lc, oracle_mod):
     """Several filters used from several threads at once (re-entrancy)."""
     g1, g2 = load_golden("random_int24"), load_golden("sine")
