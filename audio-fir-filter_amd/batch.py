@@ -110,11 +110,12 @@ class Backend:
         self.zero_peaks(clear)
 
     def filter_normalize_prev(self, xw, x_lo, x_hi, n, nch, yw, start, end, peaks, slot: int,
-                              prev_yw, prev_count: int, prev_slot: int, force: bool):
-        """filter, plus the previous shard's per-file normalize (slot prev_slot,
-        final already).  A device backend fuses the two into one launch."""
+                              prev_yw, prev_count: int, prev_peaks, prev_slot: Optional[int], force: bool):
+        """filter, plus an earlier shard's per-file normalize (its peak in
+        prev_peaks[prev_slot], final already; prev_slot None = max over all
+        slots).  A device backend fuses the two into one launch."""
         self.filter(xw, x_lo, x_hi, n, nch, yw, start, end, peaks, slot)
-        self.normalize(prev_yw, nch, prev_count, peaks, prev_slot, force)
+        self.normalize(prev_yw, nch, prev_count, prev_peaks, prev_slot, force)
 
     def new_peaks(self, nfiles: int):
         raise NotImplementedError
@@ -143,12 +144,26 @@ class BatchRunner:
     lanes (its own stream, output buffers and peak vectors), so on the device
     a step's first segments run on the CUs the previous step's last round
     leaves idle.  Steps of one lane stay in order; results() is the latest
-    step's outputs."""
+    step's outputs.
+
+    Where the normalize goes (ProcessFile.cp:91-101, per file):
+      * no peak exchange: a file's peak is final when its own filter is done,
+        so its normalize rides in the NEXT shard's filter launch of the same
+        step (fuse); only the last shard's runs as a pass of its own;
+      * with a peak exchange (config 5 over ranks, split files, global scope):
+        every normalize must wait for the all-reduce, so each shard's normalize
+        rides in the same shard's filter launch of the lane's NEXT step
+        (defer).  A step then is filter launches + the all-reduce, with no
+        pass of its own; the outputs alternate between two buffer sets per
+        lane, and results() / close() run the normalizes still pending
+        (flush) before anyone reads the outputs.
+    force_exchange runs the all-reduce even where the plan needs none (world
+    1: it exercises the collective on the device, RCCL included)."""
 
     def __init__(self, backend: Backend, rank: int, world: int, nframes: Sequence[int], nch: int,
                  half: int, normalize: bool = False, peak_scope: str = "file",
                  allreduce_max: Optional[Callable] = None, lanes: int = 1,
-                 fuse_normalize: bool = True):
+                 fuse_normalize: bool = True, force_exchange: bool = False):
         if peak_scope not in ("file", "global"):
             raise ValueError("peak_scope must be 'file' or 'global'")
         if lanes < 1:
@@ -166,7 +181,7 @@ class BatchRunner:
         # over its ranks), for the batch-global variant, and with --normalize
         # (config 5: every rank learns every file's peak; zeros elsewhere keep
         # each file's own peak, ProcessFile.cp:92-101)
-        self.exchange = world > 1 and (split or peak_scope == "global" or normalize)
+        self.exchange = force_exchange or (world > 1 and (split or peak_scope == "global" or normalize))
         if self.exchange and allreduce_max is None:
             raise ValueError("this plan needs a MAX all-reduce of the peak vector")
         self.allreduce_max = allreduce_max
@@ -175,24 +190,31 @@ class BatchRunner:
         # (Backend.filter_normalize_prev) and only the last shard's runs as a
         # pass of its own.  With an exchange every normalize waits for it.
         self.fuse = fuse_normalize and not self.exchange and peak_scope == "file"
-        # per lane, two peak vectors alternating by step: a step's last
-        # normalize launch also zeroes the other one for the lane's next step,
-        # so no separate reset launch sits in the step
+        # With an exchange, each normalize rides in the lane's next step instead.
+        self.defer = fuse_normalize and self.exchange
+        # Per lane, peak vectors rotating by step: a step's last normalize
+        # launch (or, deferred, a reset after the all-reduce) zeroes the next
+        # step's, so no separate reset launch sits in a step.  Deferred, a
+        # step's vector is still read by the next step: three in rotation.
         self.lanes = lanes
-        self._peak_bufs = [[backend.new_peaks(len(self.nframes)) for _ in range(2)]
+        self._nvec = 3 if self.defer else 2
+        self._nsets = 2 if self.defer else 1  # output buffer sets per lane
+        self._peak_bufs = [[backend.new_peaks(len(self.nframes)) for _ in range(self._nvec)]
                            for _ in range(lanes)]
-        self._cur = [0] * lanes
+        self._steps = [0] * lanes  # steps issued per lane since prepare()
+        self._pending = [None] * lanes  # defer: (outputs, peaks) of the lane's last step, not normalized
         self._lane = 0
         self._last = 0
         self.peaks = self._peak_bufs[0][0]  # the most recent step's per-file peaks
         self.inputs = []
         self.outputs = []
-        self._outs = [[] for _ in range(lanes)]
+        self._outs = [[[] for _ in range(self._nsets)] for _ in range(lanes)]
 
     def prepare(self, get_window: Callable):
         """get_window(file, x_lo, x_hi) -> [nch][x_hi - x_lo] float32 samples."""
         self.inputs = []
-        self._outs = [[] for _ in range(self.lanes)]
+        self._outs = [[[] for _ in range(self._nsets)] for _ in range(self.lanes)]
+        self._pending = [None] * self.lanes
         self.b.join_lanes()  # a re-prepare waits for steps still in flight on any lane
         self.b.set_lane(0)
         for bufs in self._peak_bufs:
@@ -203,69 +225,101 @@ class BatchRunner:
             lo, hi = self.b.window(n, sh.start, sh.end, self.half)
             xw = self.b.upload(sh.file, get_window(sh.file, lo, hi), lo, hi)
             self.inputs.append((xw, lo, hi))
-            for lane, outs in enumerate(self._outs):
-                outs.append(self.b.alloc_out(self.nch, sh.end - sh.start))
+            for lane, sets in enumerate(self._outs):
                 self.b.retain(xw, lane)
-                self.b.retain(outs[-1], lane)
+                for outs in sets:
+                    outs.append(self.b.alloc_out(self.nch, sh.end - sh.start))
+                    self.b.retain(outs[-1], lane)
         for lane, bufs in enumerate(self._peak_bufs):
             for pk in bufs:
                 self.b.retain(pk, lane)
-        self.outputs = self._outs[0]
+        self.outputs = self._outs[0][0]
         self.b.join_lanes()
-        self._cur = [0] * self.lanes
+        self._steps = [0] * self.lanes
         self._lane = 0
         self._last = 0
+
+    def output_buffer(self, lane: int, index: int, which: int = 0):
+        """Output handle of shard `index` in buffer set `which` of `lane`."""
+        return self._outs[lane][which][index]
+
+    def _slot(self, sh: Shard) -> Optional[int]:
+        return None if self.scope == "global" else sh.file
 
     def step(self):
         lane = self._lane
         self.b.set_lane(lane)
-        outputs = self._outs[lane]
-        peaks = self._peak_bufs[lane][self._cur[lane]]      # zero (prepare, or the lane's previous step)
-        nxt = self._peak_bufs[lane][1 - self._cur[lane]]
+        k = self._steps[lane]
+        outputs = self._outs[lane][k % self._nsets]
+        peaks = self._peak_bufs[lane][k % self._nvec]        # zero (prepare, or the lane's previous step)
+        nxt = self._peak_bufs[lane][(k + 1) % self._nvec]    # the lane's next step's: zeroed by this step
+        pend = self._pending[lane]
         prev = None
-        for sh, (xw, lo, hi), yw in zip(self.shards, self.inputs, outputs):
-            if self.fuse and prev is not None:
-                psh, pyw = prev
-                self.b.filter_normalize_prev(xw, lo, hi, self.nframes[sh.file], self.nch, yw, sh.start,
-                                             sh.end, peaks, sh.file, pyw, psh.end - psh.start, psh.file,
+        for i, (sh, (xw, lo, hi), yw) in enumerate(zip(self.shards, self.inputs, outputs)):
+            n = self.nframes[sh.file]
+            if pend is not None:
+                # deferred: shard i's normalize of the lane's previous step
+                # (peaks final: that step's all-reduce ran before on this lane)
+                self.b.filter_normalize_prev(xw, lo, hi, n, self.nch, yw, sh.start, sh.end, peaks, sh.file,
+                                             pend[0][i], sh.end - sh.start, pend[1], self._slot(sh),
                                              self.normalize)
+            elif self.fuse and prev is not None:
+                psh, pyw = prev
+                self.b.filter_normalize_prev(xw, lo, hi, n, self.nch, yw, sh.start, sh.end, peaks, sh.file,
+                                             pyw, psh.end - psh.start, peaks, psh.file, self.normalize)
             else:
-                self.b.filter(xw, lo, hi, self.nframes[sh.file], self.nch, yw, sh.start, sh.end,
-                              peaks, sh.file)
+                self.b.filter(xw, lo, hi, n, self.nch, yw, sh.start, sh.end, peaks, sh.file)
             prev = (sh, yw)
         if self.exchange:
             self.allreduce_max(peaks)
-        last = len(self.shards) - 1
-        for i, (sh, yw) in enumerate(zip(self.shards, outputs)):
-            if self.fuse and i < last:
-                continue  # rescaled inside the next shard's filter launch
-            slot = None if self.scope == "global" else sh.file
-            if i == last:
-                self.b.normalize_clear(yw, self.nch, sh.end - sh.start, peaks, slot, self.normalize,
-                                       nxt)
-            else:
-                self.b.normalize(yw, self.nch, sh.end - sh.start, peaks, slot, self.normalize)
-        if not self.shards:
+        if self.defer:
+            self._pending[lane] = (outputs, peaks)
             self.b.zero_peaks(nxt)
+        else:
+            last = len(self.shards) - 1
+            for i, (sh, yw) in enumerate(zip(self.shards, outputs)):
+                if self.fuse and i < last:
+                    continue  # rescaled inside the next shard's filter launch
+                if i == last:
+                    self.b.normalize_clear(yw, self.nch, sh.end - sh.start, peaks, self._slot(sh),
+                                           self.normalize, nxt)
+                else:
+                    self.b.normalize(yw, self.nch, sh.end - sh.start, peaks, self._slot(sh), self.normalize)
+            if not self.shards:
+                self.b.zero_peaks(nxt)
         self.peaks = peaks
         self.outputs = outputs
-        self._cur[lane] = 1 - self._cur[lane]
+        self._steps[lane] = k + 1
         self._last = lane
         self._lane = (lane + 1) % self.lanes
         if lane != 0:
             self.b.set_lane(0)  # the caller's stream is current again after every step
 
+    def flush(self):
+        """Run the normalizes still pending (defer: each lane's last step) as
+        passes of their own, on their lanes."""
+        for lane, pend in enumerate(self._pending):
+            if pend is None:
+                continue
+            self.b.set_lane(lane)
+            for sh, yw in zip(self.shards, pend[0]):
+                self.b.normalize(yw, self.nch, sh.end - sh.start, pend[1], self._slot(sh), self.normalize)
+            self._pending[lane] = None
+        self.b.set_lane(0)
+
     def results(self):
         """[(shard, output handle)] of the latest step.  The caller's current
         stream is made to wait for that step's lane first, so reading the
         handles there (a copy to the host, a follow-on kernel) needs no
-        device-wide synchronisation."""
+        device-wide synchronisation.  Pending (deferred) normalizes run first."""
+        self.flush()
         self.b.publish(self._last)
         return list(zip(self.shards, self.outputs))
 
     def close(self):
         """Order every lane's outstanding work before the caller's later work
         (and before the runner's buffers can be reused)."""
+        self.flush()
         self.b.join_lanes()
         for lane in range(self.lanes):
             self.b.publish(lane)
@@ -282,7 +336,10 @@ class DeviceBackend(Backend):
         # own_streams: lane 0 too gets a stream of its own (HIP graph capture
         # cannot run on the default stream; GraphedSteps); it is the current
         # stream after every step
-        self.streams = [torch.cuda.Stream(device) if own_streams else torch.cuda.current_stream(device)]
+        # the caller's stream at construction: buffers the runner allocates
+        # are allocated on it (retain, publish)
+        self.alloc_stream = torch.cuda.current_stream(device)
+        self.streams = [torch.cuda.Stream(device) if own_streams else self.alloc_stream]
         self.streams += [torch.cuda.Stream(device) for _ in range(lanes - 1)]
         self.stream = self.streams[0]
         self.sp = self.stream.cuda_stream
@@ -300,14 +357,20 @@ class DeviceBackend(Backend):
                     s.wait_stream(o)
 
     def retain(self, handle, lane):
-        # allocated on the caller's stream, written/read on a side lane: the
-        # caching allocator must not hand the block out again before that
-        # lane's work is done
-        if lane > 0:
+        # allocated on the caller's stream, written/read on another lane's
+        # stream (lanes 1.., and lane 0 too with own_streams): the caching
+        # allocator must not hand the block out again before that lane's work
+        # is done
+        if self.streams[lane] != self.alloc_stream:
             handle.record_stream(self.streams[lane])
 
     def publish(self, lane):
-        self.torch.cuda.current_stream(self.dev).wait_stream(self.streams[lane])
+        # the current stream (lane 0's after a step) and the allocation stream
+        # both wait for the lane
+        cur = self.torch.cuda.current_stream(self.dev)
+        cur.wait_stream(self.streams[lane])
+        if self.alloc_stream != cur:
+            self.alloc_stream.wait_stream(self.streams[lane])
 
     def new_peaks(self, nfiles):
         return self.torch.zeros(max(1, nfiles), dtype=self.torch.float32, device=self.dev)
@@ -337,14 +400,14 @@ class DeviceBackend(Backend):
         self.lc.normalize_dev(yw, yw.shape[1], nch, count, p, p.numel(), force, self.sp)
 
     def filter_normalize_prev(self, xw, x_lo, x_hi, n, nch, yw, start, end, peaks, slot,
-                              prev_yw, prev_count, prev_slot, force):
+                              prev_yw, prev_count, prev_peaks, prev_slot, force):
         if not prev_yw.is_contiguous() or prev_yw.shape[1] != prev_count:
             return super().filter_normalize_prev(xw, x_lo, x_hi, n, nch, yw, start, end, peaks, slot,
-                                                 prev_yw, prev_count, prev_slot, force)
+                                                 prev_yw, prev_count, prev_peaks, prev_slot, force)
+        pp = prev_peaks if prev_slot is None else prev_peaks[prev_slot:prev_slot + 1]
         self.flt.filter_window_norm_dev(xw, x_lo, x_hi, xw.shape[1], n, nch, yw, start, yw.shape[1],
                                         start, end, peaks[slot:slot + 1], 0, prev_yw,
-                                        prev_yw.numel(), peaks[prev_slot:prev_slot + 1], 1, force,
-                                        self.sp)
+                                        prev_yw.numel(), pp, pp.numel(), force, self.sp)
 
     def normalize_clear(self, yw, nch, count, peaks, slot, force, clear):
         p = peaks if slot is None else peaks[slot:slot + 1]
@@ -373,7 +436,11 @@ class GraphedSteps:
         s0 = backend.streams[0]
         if s0 == torch.cuda.default_stream(backend.dev):
             raise ValueError("lane 0 must be a stream of its own: DeviceBackend(own_streams=True)")
-        while runner._lane != 0:  # eager steps up to a round boundary: the capture starts on lane 0
+        # eager steps up to a round boundary (the capture starts on lane 0), and
+        # at least one on every lane: a partitioned filter's partial-sum scratch
+        # is sized per stream by an eager call (lcfir refuses to allocate it
+        # inside a capture, where the graph would keep a pointer it does not own)
+        while runner._lane != 0 or min(runner._steps) == 0:
             runner.step()
         self.runner, self.backend = runner, backend
         self.per_replay = 2 * runner.lanes
@@ -402,11 +469,23 @@ class GraphedSteps:
         runner._last = runner.lanes - 1
 
     def replay(self):
-        """Run per_replay steps, each graph on its lane's stream (the caller syncs)."""
+        """Run per_replay steps, each graph on its lane's stream (the caller
+        syncs).  One-graph mode: the graph is launched on lane 0's stream but
+        runs every lane's steps, so lane 0 first waits for work already queued
+        on the other lanes, and the other lanes then wait for the graph, so
+        eager steps before and after a replay stay in order on every lane."""
         torch = self.backend.torch
+        one = len(self.graphs) == 1 and len(self.backend.streams) > 1
+        s0 = self.backend.streams[0]
+        if one:
+            for s in self.backend.streams[1:]:
+                s0.wait_stream(s)
         for s, g in self.graphs:
             with torch.cuda.stream(s):
                 g.replay()
+        if one:
+            for s in self.backend.streams[1:]:
+                s.wait_stream(s0)
 
 
 def torch_allreduce_max(group=None):

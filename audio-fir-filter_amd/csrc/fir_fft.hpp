@@ -122,6 +122,15 @@ constexpr uint16_t kFftWave0C0[32] = {
 constexpr int kFftMaxTaps = 1 << 20; // longest filter (partitions of <= kFftMaxPartTaps)
 constexpr size_t kFftPairTable = (size_t)3 * kFftPairSlots * kFftNT; // double2 per pair table
 
+// Per-context choices of the FFT method (lcfir_ctx_set_fft_tuning, include/lcfir.h).
+// The defaults are the product's; tests set the others explicitly (no
+// environment variable is read anywhere in the library).
+struct FftTuning {
+    int32_t zero_phase = 1; // 1: linear-phase filters run in zero-phase form (fft_sym_eligible); 0: general table
+    int64_t chunk = 0;      // outputs per launch chunk; 0 = 2^28 (the buffer offsets' 32-bit range)
+    int64_t max_units = 0;  // units per launch; 0 = 2^31 - 1 (FftGrid's 32-bit unit index)
+};
+
 // A filter longer than one segment allows is split into `parts` equal
 // partitions of `ntaps` taps (odd, zero padded at the end), each convolved by
 // its own launch with the input offset half - p * ntaps; the launches sum in
@@ -137,44 +146,18 @@ struct FftPlan {
     uint32_t *d_task = nullptr; // [512] task words (cA, d1A, e1A, cB, d1B, e1B)
     int cus = 256;             // compute units of the plan's device (persistent grid)
     bool sym = false;          // linear-phase filter run in zero-phase form (kFftOutSym)
-    double2 *d_pair16 = nullptr; // waves16 only: fir_fft16's per-bin (a, b) table, [8][1024]
-    bool waves16 = false;         // sym + LCFIR_FFT_WAVES=16: the 16-wave kernel (fir_fft16.hpp)
+    FftTuning tune;            // the ctx's tuning when the plan was built
 };
-
-// LCFIR_FFT_WAVES=16 runs the zero-phase form on the 16-wave kernel
-// (fir_fft16.hpp: four waves per SIMD).  It is parity-exact but measured
-// 21 % slower on config 2 (+33 % VALU instructions), so this
-// file's 8-wave kernel stays the default.
-inline bool fft_use_w16() {
-    static const bool on = [] {
-        const char *e = std::getenv("LCFIR_FFT_WAVES");
-        return e && std::atoi(e) == 16;
-    }();
-    return on;
-}
-// LCFIR_FFT_WAVES=4: every form on the 4-wave kernel (fir_fft4.hpp: one wave
-// per SIMD, four columns per wave)
-inline bool fft_use_w4() {
-    static const bool on = [] {
-        const char *e = std::getenv("LCFIR_FFT_WAVES");
-        return e && std::atoi(e) == 4;
-    }();
-    return on;
-}
 
 // A filter runs in zero-phase form (kFftOutSym: real pair table, a cheaper
 // pair step) when it is one partition, half = (T-1)/2 is even (the output
 // pairs stay 8-byte aligned) and it is symmetric, h[k] = h[T-1-k], up to an
 // antisymmetric part of at most 2^-50 of its l1 norm.  Dropping that part
 // changes any output by at most 2^-50 |h|_1 max|x| -- the size of the f64
-// FFT's own rounding error.  LCFIR_FFT_SYM=0 turns the form off.
-inline bool fft_sym_eligible(const std::vector<double> &h, int parts) {
-    static const bool on = [] {
-        const char *e = std::getenv("LCFIR_FFT_SYM");
-        return !(e && e[0] == '0');
-    }();
+// FFT's own rounding error.  FftTuning::zero_phase = 0 turns the form off.
+inline bool fft_sym_eligible(const std::vector<double> &h, int parts, const FftTuning &tune) {
     const int T = (int)h.size();
-    if (!on || parts != 1 || T < 3 || ((T - 1) / 2) % 2 != 0) return false;
+    if (!tune.zero_phase || parts != 1 || T < 3 || ((T - 1) / 2) % 2 != 0) return false;
     long double anti = 0.0L, norm = 0.0L;
     for (int k = 0; k < T; ++k) {
         anti += fabsl(((long double)h[(size_t)k] - (long double)h[(size_t)(T - 1 - k)]) * 0.5L);
@@ -1142,12 +1125,6 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     }
 }
 
-} // namespace lcfir
-
-#include "fir_fft16.hpp"
-#include "fir_fft4.hpp"
-
-namespace lcfir {
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
@@ -1185,7 +1162,7 @@ inline void fft_ld(std::vector<long double> &re, std::vector<long double> &im) {
 } // namespace detail
 
 
-inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, hipStream_t s,
+inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, const FftTuning &tune, hipStream_t s,
                            std::string &err) {
     if (!fft_supported(ntaps)) {
         err = "tap count outside the FFT method's range";
@@ -1200,7 +1177,7 @@ inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, hipSt
     }
     const int parts = fft_partition_count(ntaps);
     const int tp = parts == 1 ? ntaps : fft_partition_taps(ntaps, parts);
-    const bool sym = fft_sym_eligible(taps, parts);
+    const bool sym = fft_sym_eligible(taps, parts, tune);
     const long double scale = 1.0L / (4.0L * (long double)kFftM);
     const long double two_pi = 6.283185307179586476925286766559L;
     // pair tables in consumption order: slot i of thread t holds bin k_i of
@@ -1265,23 +1242,6 @@ inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, hipSt
             }
         }
     }
-    // fir_fft16's zero-phase table: per bin k = w + 16 (lane + 64 e2) of thread
-    // t = 64 w + lane, slot e2: conj(V_k) = conj(Z_k) a + Z_{M-k} (-i b) with
-    // a = 2S + 2D Im W_L^k, b = 2D Re W_L^k (the P-role form above, valid for
-    // every bin; G is the last partition's spectrum, sym implies one)
-    std::vector<double2> pair16;
-    const bool use16 = sym && fft_use_w16();
-    if (use16) {
-        pair16.resize(kFft16PairTable);
-        for (int t = 0; t < kFft16NT; ++t)
-            for (int e2 = 0; e2 < 8; ++e2) {
-                const int k = (t >> 6) + 16 * ((t & 63) + 64 * e2);
-                const long double gr = re[(size_t)k] * scale, hr = re[(size_t)(kFftM - k)] * scale;
-                const long double sr = gr + hr, dr = gr - hr;
-                const long double a = -two_pi * (long double)k / (long double)kFftL;
-                pair16[(size_t)e2 * kFft16NT + (size_t)t] = cplx(2 * sr + 2 * dr * sinl(a), 2 * dr * cosl(a));
-            }
-    }
     std::vector<double2> tw((size_t)kFftTw);
     for (int i = 0; i < 512; ++i) {
         const long double a = -two_pi * (long double)i / 8192.0L;
@@ -1294,15 +1254,8 @@ inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, hipSt
     // stream-ordered on the ctx's own stream s (freed the same way, fft_plan_free)
     if (hipMallocAsync(reinterpret_cast<void **>(&plan.d_pair), sizeof(double2) * pair.size(), s) != hipSuccess ||
         hipMallocAsync(reinterpret_cast<void **>(&plan.d_tw), sizeof(double2) * tw.size(), s) != hipSuccess ||
-        hipMallocAsync(reinterpret_cast<void **>(&plan.d_task), sizeof(uint32_t) * task.size(), s) != hipSuccess ||
-        (use16 && hipMallocAsync(reinterpret_cast<void **>(&plan.d_pair16), sizeof(double2) * pair16.size(), s) !=
-                    hipSuccess)) {
+        hipMallocAsync(reinterpret_cast<void **>(&plan.d_task), sizeof(uint32_t) * task.size(), s) != hipSuccess) {
         err = "hipMallocAsync for the FFT plan failed";
-        return false;
-    }
-    if (use16 && hipMemcpyAsync(plan.d_pair16, pair16.data(), sizeof(double2) * pair16.size(),
-                              hipMemcpyHostToDevice, s) != hipSuccess) {
-        err = "FFT plan upload failed";
         return false;
     }
     if (hipMemcpyAsync(plan.d_pair, pair.data(), sizeof(double2) * pair.size(), hipMemcpyHostToDevice, s) !=
@@ -1323,7 +1276,7 @@ inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, hipSt
     plan.ntaps = tp;
     plan.parts = parts;
     plan.sym = sym;
-    plan.waves16 = use16;
+    plan.tune = tune;
     plan.B = kFftL - tp + 1;
     plan.c8 = std::move(c8);
     plan.ready = true;
@@ -1333,31 +1286,15 @@ inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, hipSt
 // work array + twiddles + one f32 peak slot per wave
 constexpr size_t fft_lds_bytes() { return sizeof(double2) * (size_t)(kFftM + kFftTw) + 4 * (kFftNT / 64); }
 
-// workgroups per CU the persistent grid assumes (137 KiB of LDS each: one);
-// LCFIR_FFT_BLOCKS_PER_CU overrides for experiments
-inline int fft_blocks_per_cu() {
-    static const int v = [] {
-        const char *e = std::getenv("LCFIR_FFT_BLOCKS_PER_CU");
-        const int b = e ? std::atoi(e) : 1;
-        return b > 0 ? b : 1;
-    }();
-    return v;
-}
-
 // Outputs per launch.  The kernel addresses samples and outputs through raw
 // buffer resources with 32-bit byte offsets (and 0x80000000 as its "drop this
 // store" offset), so every launch's input window and output range must stay
 // well under 2 GiB: longer ranges are split into chunks, each with its own
 // narrowed input window.  Overlap-save is exact under any segmentation, and
 // an output only needs x[out - half, out + half], inside its chunk's window.
-// LCFIR_FFT_CHUNK overrides (tests exercise the chunk seams with small values).
-inline int64_t fft_chunk() {
-    static const int64_t v = [] {
-        const char *e = std::getenv("LCFIR_FFT_CHUNK");
-        const long long c = e ? std::atoll(e) : 0;
-        return c >= 4096 ? (int64_t)c : ((int64_t)1 << 28);
-    }();
-    return v;
+// FftTuning::chunk lowers it (tests exercise the chunk seams with small values).
+inline int64_t fft_chunk(const FftPlan &plan) {
+    return plan.tune.chunk >= 4096 ? plan.tune.chunk : ((int64_t)1 << 28);
 }
 
 template <int kOut, bool kNrm = false>
@@ -1366,15 +1303,12 @@ inline bool fft_launch_one(const FftPlan &plan, const DirectParams &q, int part,
     static const bool attr = [] {
         return hipFuncSetAttribute(reinterpret_cast<const void *>(&fir_fft_f64_kernel<kOut, kNrm>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)fft_lds_bytes()) == hipSuccess &&
-               hipFuncSetAttribute(reinterpret_cast<const void *>(&fir_fft4_f64_kernel<kOut>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)fft_lds_bytes()) == hipSuccess;
     }();
     (void)attr;
     const int64_t nseg = (q.end - q.seg0 + plan.B - 1) / plan.B;
     const int64_t units = nseg * nch; // < 2^31 (fft_launch)
-    const int64_t grid = std::min<int64_t>(units, (int64_t)plan.cus * fft_blocks_per_cu());
+    const int64_t grid = std::min<int64_t>(units, (int64_t)plan.cus); // one 137 KiB workgroup per CU
     const FftGrid gd = fft_grid(nseg, units);
     if constexpr (kNrm) {
         // the previous file's floats over this launch's units, whole 1 024-float
@@ -1388,11 +1322,7 @@ inline bool fft_launch_one(const FftPlan &plan, const DirectParams &q, int part,
         hipLaunchKernelGGL((fir_fft_f64_kernel<kOut, true>), dim3((unsigned)grid), dim3(kFftNT), fft_lds_bytes(),
                            s, q, plan.d_pair + (size_t)part * kFftPairTable, plan.d_tw, plan.d_task, plan.B, gd,
                            plan.c8[(size_t)part], nrm);
-    } else if (fft_use_w4())
-        hipLaunchKernelGGL(fir_fft4_f64_kernel<kOut>, dim3((unsigned)grid), dim3(kFft4NT), fft_lds_bytes(), s, q,
-                           plan.d_pair + (size_t)part * kFftPairTable, plan.d_tw, plan.d_task, plan.B, gd,
-                           plan.c8[(size_t)part]);
-    else
+    } else
         hipLaunchKernelGGL((fir_fft_f64_kernel<kOut, false>), dim3((unsigned)grid), dim3(kFftNT), fft_lds_bytes(),
                            s, q, plan.d_pair + (size_t)part * kFftPairTable, plan.d_tw, plan.d_task, plan.B, gd,
                            plan.c8[(size_t)part], FftNrm{});
@@ -1404,29 +1334,10 @@ inline bool fft_launch_one(const FftPlan &plan, const DirectParams &q, int part,
     return true;
 }
 
-inline bool fft16_launch(const FftPlan &plan, const DirectParams &q, int nch, hipStream_t s, std::string &err) {
-    static const bool attr = [] {
-        return hipFuncSetAttribute(reinterpret_cast<const void *>(&fir_fft16_f64_kernel<kFftOutSym>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)fft16_lds_bytes()) == hipSuccess;
-    }();
-    (void)attr;
-    const int64_t nseg = (q.end - q.seg0 + plan.B - 1) / plan.B;
-    const int64_t units = nseg * nch; // < 2^31 (fft_launch)
-    const int64_t grid = std::min<int64_t>(units, (int64_t)plan.cus);
-    hipLaunchKernelGGL(fir_fft16_f64_kernel<kFftOutSym>, dim3((unsigned)grid), dim3(kFft16NT), fft16_lds_bytes(), s, q,
-                       plan.d_pair16, plan.d_tw, plan.B, fft_grid(nseg, units));
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) {
-        err = hipGetErrorString(e);
-        return false;
-    }
-    return true;
-}
-
 // Partitioned filters (plan.parts > 1) keep f64 partial sums: 2^26 outputs
 // per chunk keep the scratch's byte offsets inside the 32-bit buffer range.
 inline int64_t fft_chunk_outputs(const FftPlan &plan) {
-    return plan.parts == 1 ? fft_chunk() : std::min<int64_t>(fft_chunk(), (int64_t)1 << 26);
+    return plan.parts == 1 ? fft_chunk(plan) : std::min<int64_t>(fft_chunk(plan), (int64_t)1 << 26);
 }
 // The segment grid is anchored at output 0 of the channel: segment s covers
 // outputs [s B, (s + 1) B) whatever range a call asks for, and launch chunks
@@ -1467,15 +1378,11 @@ inline size_t fft_scratch_doubles(const FftPlan &plan, const DirectParams &p, in
 // filter's own (the plan holds the partitioning); a partitioned filter needs
 // p.y64 = fft_scratch_doubles() of scratch, owned by the caller's stream.
 // Largest unit count of one launch: 2^31 - 1 (FftGrid's 32-bit unit index);
-// LCFIR_FFT_MAX_UNITS lowers it (tests exercise the channel-group split with
+// FftTuning::max_units lowers it (tests exercise the channel-group split with
 // small values)
-inline int64_t fft_max_units() {
-    static const int64_t v = [] {
-        const char *e = std::getenv("LCFIR_FFT_MAX_UNITS");
-        const long long m = e ? std::atoll(e) : 0;
-        return m >= 1 && m < (1LL << 31) ? (int64_t)m : (((int64_t)1 << 31) - 1);
-    }();
-    return v;
+inline int64_t fft_max_units(const FftPlan &plan) {
+    const int64_t m = plan.tune.max_units;
+    return m >= 1 && m < ((int64_t)1 << 31) ? m : (((int64_t)1 << 31) - 1);
 }
 inline bool fft_launch_group(const FftPlan &plan, const DirectParams &p, int nch, hipStream_t s,
                              std::string &err, const FftNrm *nrm);
@@ -1485,11 +1392,11 @@ inline bool fft_launch_group(const FftPlan &plan, const DirectParams &p, int nch
 // The first launch (the one that carries it) must spread the previous
 // file's floats at <= kNrmK x 1 024 per unit.
 inline bool fft_nrm_fusable(const FftPlan &plan, const FftNrm &nrm, const DirectParams &p, int nch) {
-    if (plan.parts != 1 || plan.waves16 || fft_use_w4() || !nrm.y || !nrm.peak || nrm.npeak < 1 ||
+    if (plan.parts != 1 || !nrm.y || !nrm.peak || nrm.npeak < 1 ||
         (reinterpret_cast<uintptr_t>(nrm.y) & 15) != 0 || p.end <= p.start || nch <= 0)
         return false;
     const int64_t nseg = fft_first_nseg(plan, p);
-    const int64_t group = std::max<int64_t>(1, std::min<int64_t>(nch, fft_max_units() / nseg));
+    const int64_t group = std::max<int64_t>(1, std::min<int64_t>(nch, fft_max_units(plan) / nseg));
     const int64_t units = nseg * group;
     const int64_t per = (nrm.count + units - 1) / units;
     return (per + 1023) / 1024 <= kNrmK;
@@ -1510,7 +1417,7 @@ inline bool fft_launch(const FftPlan &plan, const DirectParams &p, int nch, hipS
     // launch's channels x segments below 2^31 (the partial-sum scratch is
     // reused by each group in stream order)
     const int64_t nseg = fft_first_nseg(plan, p);
-    const int group = (int)std::max<int64_t>(1, std::min<int64_t>(nch, fft_max_units() / nseg));
+    const int group = (int)std::max<int64_t>(1, std::min<int64_t>(nch, fft_max_units(plan) / nseg));
     for (int c0 = 0; c0 < nch; c0 += group) {
         DirectParams q = p;
         q.x = p.x + (int64_t)c0 * p.x_stride;
@@ -1539,10 +1446,6 @@ inline bool fft_launch_group(const FftPlan &plan, const DirectParams &p, int nch
         q.x_hi = hi;
         q.ntaps = plan.ntaps;
         if (plan.parts == 1) {
-            if (plan.waves16) {
-                if (!fft16_launch(plan, q, nch, s, err)) return false;
-                continue;
-            }
             // the first chunk's launch carries the fused normalize
             const bool fuse = nrm && cs == g0;
             bool ok;
@@ -1578,7 +1481,6 @@ inline void fft_plan_free(FftPlan &plan, hipStream_t s) {
     if (plan.d_pair) (void)hipFreeAsync(plan.d_pair, s);
     if (plan.d_tw) (void)hipFreeAsync(plan.d_tw, s);
     if (plan.d_task) (void)hipFreeAsync(plan.d_task, s);
-    if (plan.d_pair16) (void)hipFreeAsync(plan.d_pair16, s);
     plan = FftPlan{};
 }
 

@@ -38,6 +38,7 @@ struct lcfir_ctx {
     int method = LCFIR_METHOD_AUTO;
     double *d_taps = nullptr;
     lcfir::FftPlan fft; // frequency-domain filter, built lazily
+    lcfir::FftTuning tune; // lcfir_ctx_set_fft_tuning; the next plan build uses it
     std::mutex fft_mu;
     // The ctx's device memory is stream-ordered (hipMallocAsync on `own`), so
     // destroying a ctx frees it without hipFree's implicit device-wide
@@ -51,9 +52,11 @@ struct lcfir_ctx {
     struct Scratch {
         hipStream_t stream;
         double *p;
-        size_t cap; // doubles
+        size_t cap;    // doubles
+        bool captured; // a HIP graph captured on `stream` holds p: never freed before lcfir_ctx_destroy
     };
     std::vector<Scratch> scratch;
+    std::vector<double *> retired; // outgrown scratch that a captured graph may still use
 };
 
 namespace {
@@ -123,7 +126,7 @@ int ensure_fft(lcfir_ctx *ctx) {
     std::lock_guard<std::mutex> lk(ctx->fft_mu);
     if (ctx->fft.ready) return LCFIR_OK;
     std::string err;
-    if (!lcfir::fft_plan_build(ctx->fft, ctx->d_taps, ctx->ntaps, ctx->own, err))
+    if (!lcfir::fft_plan_build(ctx->fft, ctx->d_taps, ctx->ntaps, ctx->tune, ctx->own, err))
         return fail(LCFIR_EDEVICE, "fft plan: %s", err.c_str());
     return LCFIR_OK;
 }
@@ -138,23 +141,41 @@ void note_stream(lcfir_ctx *ctx, hipStream_t s) {
 
 // The partial-sum scratch of stream s, at least `need` doubles, allocated and
 // (when it grows) freed in s's own order: no device-wide synchronisation.
-double *stream_scratch(lcfir_ctx *ctx, hipStream_t s, size_t need) {
+// Under HIP graph capture the scratch must already be large enough (an eager
+// call of the same shape on s sizes it): a graph keeps the raw pointer, so an
+// allocation made inside the capture, or a later growth that freed the
+// captured buffer, would leave the graph writing freed memory.  A buffer a
+// graph captured is retired on growth, not freed (lcfir_ctx_destroy frees it).
+double *stream_scratch(lcfir_ctx *ctx, hipStream_t s, size_t need, bool &capture_error) {
+    capture_error = false;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) != hipSuccess) cs = hipStreamCaptureStatusNone;
+    const bool capturing = cs == hipStreamCaptureStatusActive;
     std::lock_guard<std::mutex> lk(ctx->streams_mu);
     lcfir_ctx::Scratch *slot = nullptr;
     for (auto &e : ctx->scratch)
         if (e.stream == s) slot = &e;
     if (!slot) {
-        ctx->scratch.push_back({s, nullptr, 0});
+        ctx->scratch.push_back({s, nullptr, 0, false});
         slot = &ctx->scratch.back();
     }
     if (slot->cap < need) {
-        if (slot->p) (void)hipFreeAsync(slot->p, s);
+        if (capturing) {
+            capture_error = true;
+            return nullptr;
+        }
+        if (slot->p) {
+            if (slot->captured) ctx->retired.push_back(slot->p);
+            else (void)hipFreeAsync(slot->p, s);
+        }
         slot->p = nullptr;
         slot->cap = 0;
+        slot->captured = false;
         if (hipMallocAsync(reinterpret_cast<void **>(&slot->p), need * sizeof(double), s) != hipSuccess)
             return nullptr;
         slot->cap = need;
     }
+    if (capturing) slot->captured = true;
     return slot->p;
 }
 
@@ -164,12 +185,15 @@ int launch_normalize(float *d_y, int64_t stride, int32_t nch, int64_t n, const u
 // Run the filter for outputs [start, end) of nch channels.  x/y geometry as
 // in DirectParams.  nrm (nullable): a previous file's normalize, fused into
 // the FFT launch where fft_nrm_fusable, else run as its own pass afterwards.
+// track_stream: remember s for lcfir_ctx_destroy's wait (false for the
+// staging streams of lcfir_apply_range, which synchronises its stream before
+// returning and may destroy it later, lcfir_staging_release).
 int run_filter(lcfir_ctx *ctx, lcfir::DirectParams p, int nch, hipStream_t s,
-               const lcfir::FftNrm *nrm = nullptr) {
+               const lcfir::FftNrm *nrm = nullptr, bool track_stream = true) {
     p.taps = ctx->d_taps;
     p.ntaps = ctx->ntaps;
     p.half = ctx->half;
-    note_stream(ctx, s);
+    if (track_stream) note_stream(ctx, s);
     const int m = resolve_method(ctx);
     if (m == LCFIR_METHOD_FFT) {
         int rc = ensure_fft(ctx);
@@ -177,7 +201,11 @@ int run_filter(lcfir_ctx *ctx, lcfir::DirectParams p, int nch, hipStream_t s,
         std::string err;
         if (ctx->fft.parts > 1) {
             const size_t need = lcfir::fft_scratch_doubles(ctx->fft, p, nch);
-            p.y64 = stream_scratch(ctx, s, need);
+            bool capture_error = false;
+            p.y64 = stream_scratch(ctx, s, need, capture_error);
+            if (capture_error)
+                return fail(LCFIR_EINVAL, "partial-sum scratch of %zu doubles is not allocated on this stream: run "
+                            "an eager call of this shape on it before HIP graph capture", need);
             if (!p.y64) return fail(LCFIR_ENOMEM, "partial-sum scratch of %zu doubles", need);
         }
         const bool fuse = nrm && lcfir::fft_nrm_fusable(ctx->fft, *nrm, p, nch);
@@ -355,6 +383,7 @@ int lcfir_ctx_destroy(lcfir_ctx *ctx) {
     for (hipStream_t s : ctx->used) (void)hipStreamSynchronize(s);
     for (auto &e : ctx->scratch)
         if (e.p) (void)hipFreeAsync(e.p, ctx->own);
+    for (double *p : ctx->retired) (void)hipFreeAsync(p, ctx->own);
     lcfir::fft_plan_free(ctx->fft, ctx->own);
     if (ctx->d_taps) (void)hipFreeAsync(ctx->d_taps, ctx->own);
     if (ctx->own) {
@@ -394,13 +423,42 @@ int lcfir_ctx_ntaps(const lcfir_ctx *ctx, int32_t *ntaps) {
     return LCFIR_OK;
 }
 
-int lcfir_ctx_fft_waves(lcfir_ctx *ctx, int32_t *waves) {
-    if (!ctx || !waves) return fail(LCFIR_EINVAL, "null argument");
-    *waves = 0;
+int lcfir_ctx_fft_info(lcfir_ctx *ctx, int32_t *seg_len, int32_t *parts, int32_t *zero_phase) {
+    if (!ctx || !seg_len || !parts || !zero_phase) return fail(LCFIR_EINVAL, "null argument");
+    *seg_len = *parts = *zero_phase = 0;
     if (!lcfir::fft_supported(ctx->ntaps)) return LCFIR_OK;
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return fail(LCFIR_EDEVICE, "hipSetDevice(%d) failed", ctx->device);
     const int rc = ensure_fft(ctx);
     if (rc != LCFIR_OK) return rc;
-    *waves = ctx->fft.waves16 ? lcfir::kFft16NT / 64 : lcfir::fft_use_w4() ? lcfir::kFft4NT / 64 : lcfir::kFftNT / 64;
+    *seg_len = lcfir::kFftL;
+    *parts = ctx->fft.parts;
+    *zero_phase = ctx->fft.sym ? 1 : 0;
+    return LCFIR_OK;
+}
+
+int lcfir_ctx_set_fft_tuning(lcfir_ctx *ctx, int32_t seg_len, int32_t zero_phase, int64_t chunk,
+                             int64_t max_units) {
+    if (!ctx) return fail(LCFIR_EINVAL, "ctx is null");
+    if (seg_len != 0 && seg_len != lcfir::kFftL)
+        return fail(LCFIR_EINVAL, "segment length %d not supported (0 or %d)", seg_len, lcfir::kFftL);
+    if (zero_phase != 0 && zero_phase != 1) return fail(LCFIR_EINVAL, "zero_phase must be 0 or 1");
+    if (chunk != 0 && chunk < 4096) return fail(LCFIR_EINVAL, "chunk must be 0 or >= 4096 outputs");
+    if (max_units < 0 || max_units >= ((int64_t)1 << 31)) return fail(LCFIR_EINVAL, "max_units out of range");
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return fail(LCFIR_EDEVICE, "hipSetDevice(%d) failed", ctx->device);
+    std::lock_guard<std::mutex> lk(ctx->fft_mu);
+    // launches already queued may still read the old plan's tables: wait for
+    // them, then free the plan; the next launch builds one with the new tuning
+    {
+        std::lock_guard<std::mutex> lk2(ctx->streams_mu);
+        for (hipStream_t s : ctx->used) (void)hipStreamSynchronize(s);
+    }
+    lcfir::fft_plan_free(ctx->fft, ctx->own);
+    LCFIR_HIP(hipStreamSynchronize(ctx->own));
+    ctx->tune.zero_phase = zero_phase;
+    ctx->tune.chunk = chunk;
+    ctx->tune.max_units = max_units;
     return LCFIR_OK;
 }
 
@@ -471,7 +529,7 @@ int lcfir_apply_range(lcfir_ctx *ctx, const float *x, int64_t n, float *y, int64
         p.start = start;
         p.end = end;
         p.peak = nullptr;
-        rc = run_filter(ctx, p, 1, st->stream);
+        rc = run_filter(ctx, p, 1, st->stream, nullptr, /*track_stream=*/false);
     }
     if (!rc) {
         if (hipMemcpyAsync(y + start, st->d_y, sizeof(float) * (size_t)(end - start),

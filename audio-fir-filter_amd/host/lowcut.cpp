@@ -7,7 +7,16 @@
 // Options as main.cp:42-56: -f/--frequency (15), -s/--slope (10),
 // -n/--normalize, -v/--verbose, -t/--threads (accepted; one device launch
 // covers a channel), -O/--overwrite, -h/--help.  Extensions: --method
-// auto|direct|fft, --device N, --info (print the parsed format, no GPU).
+// auto|direct|fft, --devices LIST (default: every visible GPU) / --device N,
+// --info (print the parsed format, no GPU), --plan (print the file-to-GPU
+// dealing, no GPU).
+//
+// A batch (scenario 2, main.cp:132-147) is dealt round-robin over the
+// devices, one file per GPU at a time (BASELINE.json north_star: "shard one
+// file per GPU"): file i goes to GPU stage i mod D, each stage with its own
+// filter contexts, streams and two pipeline slots.  Each file's normalize
+// stays on its own GPU (the peak is per file, ProcessFile.cp:91-101), so no
+// collective is needed; outputs are written in input order.
 // Scenario checks and their errors follow main.cp:84-151; errors exit with
 // EXIT_FAILURE after printing the message (main.cp:153-164).
 //
@@ -59,9 +68,30 @@ struct Options {
     bool info = false;
     bool timing = false;
     int method = LCFIR_METHOD_AUTO;
-    int device = 0;
+    std::vector<int> devices; // empty: every visible device
+    bool plan = false;
     std::vector<std::string> paths;
 };
+
+// "all" or a comma-separated list of device ordinals ("0,0" runs two GPU
+// stages on one device)
+std::vector<int> parse_devices(const std::string &v) {
+    std::vector<int> out;
+    if (v == "all") return out;
+    size_t i = 0;
+    while (i <= v.size()) {
+        const size_t j = std::min(v.find(',', i), v.size());
+        const std::string t = v.substr(i, j - i);
+        if (t.empty() || t.find_first_not_of("0123456789") != std::string::npos)
+            throw UsageError("bad --devices list: " + v);
+        out.push_back(std::stoi(t));
+        i = j + 1;
+    }
+    return out;
+}
+
+// GPU stage of file i in a batch dealt over `stages` stages: round-robin
+size_t stage_of(size_t file_index, size_t stages) { return file_index % stages; }
 
 const char *kHelp = R"(
 Applies low-cut (high-pass) FIR filter to WAVE or AIFF file.
@@ -78,7 +108,10 @@ Options:
   -O [ --overwrite ]            Overwrite existing files.
   -h [ --help ]                 Display this help message.
   --method arg (=auto)          auto | direct | fft
-  --device arg (=0)             GPU ordinal
+  --devices arg (=all)          GPUs for a batch, e.g. 0,1,2,3 (files are dealt
+                                round-robin, one file per GPU at a time)
+  --device arg                  one GPU (= --devices arg)
+  --plan                        Print which GPU stage each file goes to and exit.
   --info                        Print each input's format and exit.
   --timing                      Print per-file read/GPU/write times and the
                                 end-to-end rate.
@@ -118,7 +151,9 @@ Options parse(int argc, char **argv) {
             std::exit(EXIT_SUCCESS);
         } else if (a == "--info") o.info = true;
         else if (a == "--timing") o.timing = true;
-        else if (a == "--device") o.device = std::stoi(val(a));
+        else if (a == "--device") o.devices = {std::stoi(val(a))};
+        else if (a == "--devices") o.devices = parse_devices(val(a));
+        else if (a == "--plan") o.plan = true;
         else if (a == "--method") {
             const std::string m = val(a);
             if (m == "auto") o.method = LCFIR_METHOD_AUTO;
@@ -238,13 +273,14 @@ struct Job {
 // of a batch usually share a rate, so the taps and FFT plan are reused).
 struct FilterSet {
     const Options &o;
+    int device;
     struct Entry {
         lcfir_ctx *ctx;
         int method;
         int32_t ntaps;
     };
     std::map<double, Entry> by_rate;
-    explicit FilterSet(const Options &opt) : o(opt) {}
+    FilterSet(const Options &opt, int dev) : o(opt), device(dev) {}
     ~FilterSet() {
         for (auto &e : by_rate) lcfir_ctx_destroy(e.second.ctx);
     }
@@ -256,7 +292,7 @@ struct FilterSet {
         std::vector<double> taps((size_t)ntaps);
         check(lcfir_design_lowcut(o.freq, o.slope, fs, taps.data(), ntaps, &ntaps), "design");
         lcfir_ctx *ctx = nullptr;
-        check(lcfir_ctx_create(o.device, taps.data(), ntaps, &ctx), "lcfir_ctx_create");
+        check(lcfir_ctx_create(device, taps.data(), ntaps, &ctx), "lcfir_ctx_create");
         int method = o.method;
         if (method == LCFIR_METHOD_FFT && lcfir_ctx_set_method(ctx, method) != LCFIR_OK)
             method = LCFIR_METHOD_DIRECT; // tap count beyond the FFT segment
@@ -286,6 +322,7 @@ struct Slot {
 // folded in (:91-101, :115-117) -> D2H into
 // the same pinned buffer.  Nothing here waits on the device.
 void enqueue_file(Slot &s, Job &j, FilterSet &filters, PinnedPool &pool, const Options &o) {
+    const int dev = filters.device;
     const AudioFile &f = j.f;
     const auto &flt = filters.get(f.sample_rate);
     j.ntaps = flt.ntaps;
@@ -294,10 +331,10 @@ void enqueue_file(Slot &s, Job &j, FilterSet &filters, PinnedPool &pool, const O
     const int64_t n = f.frames;
     if (n <= 0) return;
     const size_t plane = sizeof(float) * (size_t)n * (size_t)nch;
-    void *d_raw = s.raw.get(o.device, f.data_bytes);
-    float *d_x = static_cast<float *>(s.x.get(o.device, plane));
-    float *d_y = static_cast<float *>(s.y.get(o.device, plane));
-    float *d_peak = static_cast<float *>(s.peak.get(o.device, sizeof(float) * (size_t)nch));
+    void *d_raw = s.raw.get(dev, f.data_bytes);
+    float *d_x = static_cast<float *>(s.x.get(dev, plane));
+    float *d_y = static_cast<float *>(s.y.get(dev, plane));
+    float *d_peak = static_cast<float *>(s.peak.get(dev, sizeof(float) * (size_t)nch));
     if ((size_t)nch > s.peaks_cap) {
         s.peaks_host = pool.get(sizeof(float) * (size_t)nch);
         s.peaks_cap = (size_t)nch;
@@ -316,6 +353,8 @@ void enqueue_file(Slot &s, Job &j, FilterSet &filters, PinnedPool &pool, const O
           "d2h");
 }
 
+std::mutex g_print_mu; // the GPU stages print from their own threads
+
 void finish_file(Slot &s, const Options &o) {
     check(lcfir_stream_sync(s.stream), "stream sync");
     Job &j = *s.job;
@@ -325,6 +364,7 @@ void finish_file(Slot &s, const Options &o) {
         for (int c = 0; c < j.f.channels; ++c) j.peak = std::max(j.peak, pk[c]);
     }
     if (o.verbose) {
+        std::lock_guard<std::mutex> lk(g_print_mu);
         if (j.peak > 1.0f || o.normalize) std::cout << "Doing audio normalize." << std::endl;
         std::cout << "  " << j.f.channels << " ch x " << j.f.frames << " frames, " << j.f.format_name()
                   << ", " << j.f.sample_rate << " Hz, " << j.ntaps << " taps ("
@@ -333,14 +373,68 @@ void finish_file(Slot &s, const Options &o) {
     }
 }
 
-// Reader -> GPU (2 slots) -> writer.  Files are read, filtered and written in
-// order; a failure on file k (missing input, existing output without -O,
-// unreadable container) ends the batch after files < k are written, as the
-// reference's sequential loop does (main.cp:131-146).
-void process_files(const std::vector<std::pair<fs::path, fs::path>> &todo, const Options &o) {
+// One GPU stage: its device's filter contexts, two slots (streams + buffers),
+// its own input queue; finished files go to the shared writer queue.
+struct GpuStage {
+    int device = 0;
+    Channel<Job> in{1};
+    std::exception_ptr error;
+    std::thread th;
+};
+
+void run_stage(GpuStage &st, Channel<Job> &to_writer, PinnedPool &pool, const Options &o) {
+    FilterSet filters(o, st.device);
+    Slot slots[2];
+    try {
+        for (auto &s : slots) check(lcfir_stream_create(st.device, &s.stream), "stream");
+        size_t k = 0;
+        while (auto j = st.in.pop()) {
+            Slot &s = slots[k++ % 2];
+            if (s.job) { // this slot's previous file is done once its stream drains
+                finish_file(s, o);
+                to_writer.push(std::move(*s.job));
+                s.job.reset();
+            }
+            s.t0 = Clock::now();
+            s.job.emplace(std::move(*j));
+            enqueue_file(s, *s.job, filters, pool, o);
+        }
+        for (size_t i = 0; i < 2; ++i) {
+            Slot &s = slots[k++ % 2];
+            if (!s.job) continue;
+            finish_file(s, o);
+            to_writer.push(std::move(*s.job));
+            s.job.reset();
+        }
+    } catch (...) {
+        st.error = std::current_exception();
+        while (st.in.pop()) { // keep the reader from blocking on this stage
+        }
+    }
+    for (auto &s : slots) {
+        if (s.stream) {
+            lcfir_stream_sync(s.stream);
+            lcfir_stream_destroy(s.stream);
+        }
+    }
+}
+
+// Reader -> GPU stages (file i on stage i mod D, 2 slots each) -> writer (in
+// input order).  A failure on file k (missing input, existing output without
+// -O, unreadable container, a GPU error) ends the batch after files < k are
+// written, as the reference's sequential loop does (main.cp:131-146).
+void process_files(const std::vector<std::pair<fs::path, fs::path>> &todo, const std::vector<int> &devices,
+                   const Options &o) {
     const auto t_all = Clock::now();
     PinnedPool pool;
-    Channel<Job> to_gpu(1), to_writer(2);
+    std::vector<std::unique_ptr<GpuStage>> stages;
+    for (int d : devices) {
+        stages.push_back(std::make_unique<GpuStage>());
+        stages.back()->device = d;
+    }
+    Channel<Job> to_writer(2 * stages.size());
+    std::exception_ptr read_error;
+    int64_t total_samples = 0;
     std::thread reader([&] {
         // outputs scheduled by earlier jobs: the reference's sequential loop
         // (main.cp:131-146) has written them by the time it checks a later job,
@@ -362,88 +456,66 @@ void process_files(const std::vector<std::pair<fs::path, fs::path>> &todo, const
                 j.f = lcfir_host::read_audio_file(j.in.string(),
                                                   [&](size_t n) { return pool.get(n); });
             } catch (...) {
-                j.error = std::current_exception();
-            }
-            j.t_read = seconds_since(t0);
-            const bool stop = (bool)j.error;
-            to_gpu.push(std::move(j));
-            if (stop) break;
-        }
-        to_gpu.close();
-    });
-    std::exception_ptr write_error;
-    std::thread writer([&] {
-        while (auto j = to_writer.pop()) {
-            if (write_error) continue;
-            try {
-                const auto t0 = Clock::now();
-                if (fs::exists(j->out)) fs::remove(j->out);
-                lcfir_host::write_bytes(j->out.string(), j->f.data, j->f.size);
-                j->t_write = seconds_since(t0);
-                if (o.timing)
-                    std::printf("timing %s: read %.3f s, gpu %.3f s (h2d+filter+d2h), write %.3f s, "
-                                "%lld frames x %d ch\n",
-                                j->in.filename().string().c_str(), j->t_read, j->t_gpu, j->t_write,
-                                (long long)j->f.frames, j->f.channels);
-            } catch (...) {
-                write_error = std::current_exception();
-            }
-            j->f = AudioFile{}; // the pinned buffer returns to the pool
-        }
-    });
-
-    std::exception_ptr error;
-    FilterSet filters(o);
-    Slot slots[2];
-    int64_t total_samples = 0;
-    try {
-        for (auto &s : slots) check(lcfir_stream_create(o.device, &s.stream), "stream");
-        size_t k = 0;
-        while (auto j = to_gpu.pop()) {
-            Slot &s = slots[k++ % 2];
-            if (s.job) { // this slot's previous file is done once its stream drains
-                finish_file(s, o);
-                to_writer.push(std::move(*s.job));
-                s.job.reset();
-            }
-            if (j->error) {
-                error = j->error;
+                read_error = std::current_exception();
                 break;
             }
-            std::cout << "Processing file: " << j->in.filename().string() << std::endl;
-            total_samples += j->f.frames * j->f.channels;
-            s.t0 = Clock::now();
-            s.job.emplace(std::move(*j));
-            enqueue_file(s, *s.job, filters, pool, o);
+            j.t_read = seconds_since(t0);
+            {
+                std::lock_guard<std::mutex> lk(g_print_mu);
+                std::cout << "Processing file: " << j.in.filename().string() << std::endl;
+            }
+            total_samples += j.f.frames * j.f.channels;
+            stages[stage_of(i, stages.size())]->in.push(std::move(j));
         }
-        for (size_t i = 0; i < 2; ++i) {
-            Slot &s = slots[k++ % 2];
-            if (!s.job) continue;
-            finish_file(s, o);
-            to_writer.push(std::move(*s.job));
-            s.job.reset();
+        for (auto &st : stages) st->in.close();
+    });
+    for (auto &st : stages) st->th = std::thread([&, p = st.get()] { run_stage(*p, to_writer, pool, o); });
+    std::exception_ptr write_error;
+    std::thread writer([&] {
+        std::map<size_t, Job> ready; // finished out of order across stages
+        size_t next = 0;
+        while (auto j = to_writer.pop()) {
+            const size_t idx = j->index;
+            ready.emplace(idx, std::move(*j));
+            for (auto it = ready.find(next); it != ready.end(); it = ready.find(next)) {
+                Job &w = it->second;
+                if (!write_error) {
+                    try {
+                        const auto t0 = Clock::now();
+                        if (fs::exists(w.out)) fs::remove(w.out);
+                        lcfir_host::write_bytes(w.out.string(), w.f.data, w.f.size);
+                        w.t_write = seconds_since(t0);
+                        if (o.timing) {
+                            std::lock_guard<std::mutex> lk(g_print_mu);
+                            std::printf("timing %s: read %.3f s, gpu %.3f s (h2d+filter+d2h), write %.3f s, "
+                                        "%lld frames x %d ch\n",
+                                        w.in.filename().string().c_str(), w.t_read, w.t_gpu, w.t_write,
+                                        (long long)w.f.frames, w.f.channels);
+                        }
+                    } catch (...) {
+                        write_error = std::current_exception();
+                    }
+                }
+                ready.erase(it); // the pinned buffer returns to the pool
+                ++next;
+            }
         }
-    } catch (...) {
-        if (!error) error = std::current_exception();
-    }
-    to_writer.close();
-    // drain the reader if the GPU stage stopped early
-    while (to_gpu.pop()) {
-    }
+    });
     reader.join();
+    for (auto &st : stages) st->th.join();
+    to_writer.close();
     writer.join();
-    for (auto &s : slots) {
-        if (s.stream) {
-            lcfir_stream_sync(s.stream);
-            lcfir_stream_destroy(s.stream);
-        }
-    }
-    if (error) std::rethrow_exception(error);
+    // a GPU error stops its stage; a reader error at file k comes after every
+    // file < k was dispatched (and, if no GPU error, written)
+    for (auto &st : stages)
+        if (st->error) std::rethrow_exception(st->error);
+    if (read_error) std::rethrow_exception(read_error);
     if (write_error) std::rethrow_exception(write_error);
     if (o.timing) {
         const double t = seconds_since(t_all);
-        std::printf("timing total: %zu file(s), %.3f s, %.1f Msamples/s end to end (disk + PCIe + GPU)\n",
-                    todo.size(), t, (double)total_samples / t / 1e6);
+        std::printf("timing total: %zu file(s), %zu GPU stage(s), %.3f s, %.1f Msamples/s end to end "
+                    "(disk + PCIe + GPU)\n",
+                    todo.size(), stages.size(), t, (double)total_samples / t / 1e6);
     }
 }
 
@@ -458,12 +530,39 @@ void print_info(const fs::path &in) {
     std::printf("\n");
 }
 
+// The GPU stages of this run: --devices/--device, else every visible device
+// (asks the runtime only when no list was given).
+std::vector<int> resolve_devices(const Options &o) {
+    if (!o.devices.empty()) return o.devices;
+    int n = 0;
+    check(lcfir_device_count(&n), "lcfir_device_count");
+    if (n < 1) throw std::runtime_error("no GPU visible");
+    std::vector<int> d((size_t)n);
+    for (int i = 0; i < n; ++i) d[(size_t)i] = i;
+    return d;
+}
+
+void run_or_plan(const std::vector<std::pair<fs::path, fs::path>> &todo, const Options &o) {
+    if (o.plan) {
+        // the dealing only (no GPU touched): needs an explicit device list
+        if (o.devices.empty()) throw UsageError("--plan needs --devices");
+        for (size_t i = 0; i < todo.size(); ++i) {
+            const size_t st = stage_of(i, o.devices.size());
+            std::printf("plan %s -> %s stage %zu device %d\n", todo[i].first.string().c_str(),
+                        todo[i].second.string().c_str(), st, o.devices[st]);
+        }
+        return;
+    }
+    process_files(todo, resolve_devices(o), o);
+}
+
 int run(int argc, char **argv) {
     Options o = parse(argc, argv);
     if (o.info) {
         for (const auto &p : o.paths) print_info(p);
         return EXIT_SUCCESS;
     }
+
     std::vector<fs::path> paths(o.paths.begin(), o.paths.end());
     if (paths.size() == 2) {
         // Scenario 1: input file -> output file (main.cp:84-109)
@@ -474,7 +573,7 @@ int run(int argc, char **argv) {
         if (in.extension() != out.extension())
             throw UsageError("Input and output file types (WAVE or AIFF) must be the same (extensions must match).");
         if (fs::exists(out) && !o.overwrite) throw std::runtime_error("File exists: " + out.string());
-        process_files({{in, out}}, o);
+        run_or_plan({{in, out}}, o);
     } else if (paths.size() > 2) {
         // Scenario 2: input files -> output directory (main.cp:112-147)
         const fs::path &dest = paths.back();
@@ -490,7 +589,7 @@ int run(int argc, char **argv) {
         }
         std::vector<std::pair<fs::path, fs::path>> todo;
         for (size_t i = 0; i + 1 < paths.size(); ++i) todo.emplace_back(paths[i], dest / paths[i].filename());
-        process_files(todo, o); // per-file checks run in order inside the pipeline
+        run_or_plan(todo, o); // per-file checks run in order inside the pipeline
     } else {
         throw UsageError("Invalid number of parameters. Need at least 2.");
     }

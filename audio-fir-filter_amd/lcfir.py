@@ -53,7 +53,9 @@ _SIGNATURES = {
     "lcfir_ctx_set_method": ([_ctxp, _c_int], _c_int),
     "lcfir_ctx_get_method": ([_ctxp, ctypes.POINTER(_c_int)], _c_int),
     "lcfir_ctx_half": ([_ctxp, ctypes.POINTER(_c_i32)], _c_int),
-    "lcfir_ctx_fft_waves": ([_ctxp, ctypes.POINTER(_c_i32)], _c_int),
+    "lcfir_ctx_fft_info": ([_ctxp, ctypes.POINTER(_c_i32), ctypes.POINTER(_c_i32), ctypes.POINTER(_c_i32)],
+                           _c_int),
+    "lcfir_ctx_set_fft_tuning": ([_ctxp, _c_i32, _c_i32, _c_i64, _c_i64], _c_int),
     "lcfir_ctx_ntaps": ([_ctxp, ctypes.POINTER(_c_i32)], _c_int),
     "lcfir_ctx_window": ([_ctxp, _c_i64, _c_i64, _c_i64, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i64)], _c_int),
     "lcfir_apply_range": ([_ctxp, _vp, _c_i64, _vp, _c_i64, _c_i64, PROGRESS_FN, _vp], _c_int),
@@ -197,11 +199,18 @@ class Filter:
     getMo2 = half
 
     @property
-    def fft_waves(self) -> int:
-        """Waves per workgroup of the FFT kernel this filter's plan runs (0: no FFT)."""
-        w = ctypes.c_int32()
-        _check(load().lcfir_ctx_fft_waves(self._ctx, ctypes.byref(w)))
-        return w.value
+    def fft_info(self) -> dict:
+        """The FFT plan this filter runs (lcfir_ctx_fft_info): segment length,
+        tap partitions, zero-phase form (all 0 outside the FFT's range)."""
+        L, P, Z = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        _check(load().lcfir_ctx_fft_info(self._ctx, ctypes.byref(L), ctypes.byref(P), ctypes.byref(Z)))
+        return {"seg_len": L.value, "parts": P.value, "zero_phase": bool(Z.value)}
+
+    def set_fft_tuning(self, seg_len: int = 0, zero_phase: bool = True, chunk: int = 0, max_units: int = 0):
+        """lcfir_ctx_set_fft_tuning: explicit FFT-method choices (tests run
+        every setting; the defaults are the product's)."""
+        _check(load().lcfir_ctx_set_fft_tuning(self._ctx, int(seg_len), 1 if zero_phase else 0, int(chunk),
+                                               int(max_units)))
 
     @property
     def ntaps(self) -> int:

@@ -77,11 +77,22 @@ int lcfir_ctx_set_method(lcfir_ctx *ctx, int method);
 int lcfir_ctx_get_method(const lcfir_ctx *ctx, int *method);
 int lcfir_ctx_half(const lcfir_ctx *ctx, int32_t *half); /* getMo2() */
 int lcfir_ctx_ntaps(const lcfir_ctx *ctx, int32_t *ntaps);
-/* Diagnostic: waves per workgroup of the FFT kernel this ctx's plan runs
- * (8; 16 for a linear-phase filter under LCFIR_FFT_WAVES=16; 4 under
- * LCFIR_FFT_WAVES=4); builds the plan if needed.  0 when the tap count is
- * outside the FFT method's range. */
-int lcfir_ctx_fft_waves(lcfir_ctx *ctx, int32_t *waves);
+/* Diagnostic: the FFT plan this ctx runs (built if needed): overlap-save
+ * segment length in real samples, the number of tap partitions, and whether
+ * the filter runs in zero-phase form (linear-phase taps).  All 0 when the tap
+ * count is outside the FFT method's range. */
+int lcfir_ctx_fft_info(lcfir_ctx *ctx, int32_t *seg_len, int32_t *parts, int32_t *zero_phase);
+/* Explicit FFT-method choices for this ctx (the library reads no environment
+ * variables).  seg_len: 0 = automatic by tap count, or a supported segment
+ * length; zero_phase: 1 = linear-phase filters run in zero-phase form (the
+ * default), 0 = always the general pair table; chunk: outputs per launch
+ * chunk (0 = 2^28, else >= 4096); max_units: segments x channels per launch
+ * (0 = 2^31 - 1).  Every setting gives outputs within 1 f32 ulp of every
+ * other (the tests run each); the defaults are the fast ones.  Waits for the
+ * ctx's queued launches and drops its plan; not to be called concurrently
+ * with launches on the same ctx. */
+int lcfir_ctx_set_fft_tuning(lcfir_ctx *ctx, int32_t seg_len, int32_t zero_phase, int64_t chunk,
+                             int64_t max_units);
 /* Input window [*lo, *hi) (within [0, n)) of a channel of n samples that
  * makes a call for outputs [start, end) reproduce the whole-channel call's
  * outputs bit for bit, whatever the range: the partition invariance of

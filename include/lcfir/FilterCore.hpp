@@ -32,6 +32,7 @@
 // is left untouched.
 #pragma once
 
+#include <cmath>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -126,6 +127,18 @@ template <class Sinc, class = void>
 struct sinc_traits_direct : std::false_type {};
 template <class Sinc>
 struct sinc_traits_direct<Sinc, std::enable_if_t<SincTraits<Sinc>::direct>> : std::true_type {};
+// does Sinc have getMo2() (FilterCore.h:29)?
+template <class Sinc, class = void>
+struct sinc_has_getmo2 : std::false_type {};
+template <class Sinc>
+struct sinc_has_getmo2<Sinc, std::void_t<decltype(std::declval<const Sinc &>().getMo2())>> : std::true_type {};
+// does Sinc have fms(Channel::const_iterator) (FilterCore.h:67)?
+template <class Channel, class Sinc, class = void>
+struct sinc_has_fms : std::false_type {};
+template <class Channel, class Sinc>
+struct sinc_has_fms<Channel, Sinc,
+                    std::void_t<decltype(std::declval<const Sinc &>().fms(std::declval<const Channel &>().begin()))>>
+    : std::true_type {};
 
 namespace detail {
 // A channel's samples as a pointer, through the interfaces FilterCore.h uses
@@ -146,17 +159,50 @@ inline float *out_ptr(Channel &c) {
 // sinc object, validated on reuse by getMo2() and one fms() fingerprint over a
 // fixed pseudo-random window (an object rebuilt at the same address with other
 // taps misses).
-template <class Channel, class Sinc>
-std::shared_ptr<const std::vector<double>> probe_taps(const Sinc &sinc) {
-    const int64_t half = (int64_t)sinc.getMo2();
-    if (half < 0 || half > (1 << 24)) throw Error(LCFIR_EINVAL, "sinc.getMo2() out of range");
-    const int64_t T = 2 * half + 1;
+// the fixed pseudo-random fingerprint window of T samples in [-1, 1)
+template <class Channel>
+Channel fingerprint_window(int64_t T) {
     Channel fp((size_t)T);
     uint32_t s = 0x9e3779b9u;
     for (int64_t i = 0; i < T; ++i) {
         s = s * 1664525u + 1013904223u;
         fp[(size_t)i] = (float)((int32_t)(s >> 8) - (1 << 23)) * 0x1p-23f;
     }
+    return fp;
+}
+
+// The direct path reads the taps through std::data / std::size; c_lib's
+// WindowedSinc is not vendored, so that those are exactly the 2 getMo2() + 1
+// taps in fms() order is unpinned.  Use them only if the count matches
+// getMo2() and, where fms() exists, one fms() fingerprint agrees with the
+// same dot product over data() (to 1e-12 of sum |h|: fms's accumulation
+// order is unknown); otherwise the taps are probed through fms().
+template <class Channel, class Sinc>
+bool direct_taps_valid(const Sinc &sinc, const double *h, size_t T) {
+    if (!h || T == 0) return false;
+    if constexpr (sinc_has_getmo2<Sinc>::value) {
+        const int64_t half = (int64_t)sinc.getMo2();
+        if (half < 0 || (int64_t)T != 2 * half + 1) return false;
+    }
+    if constexpr (sinc_has_fms<Channel, Sinc>::value) {
+        const Channel fp = fingerprint_window<Channel>((int64_t)T);
+        long double dot = 0.0L, norm = 0.0L;
+        for (size_t k = 0; k < T; ++k) {
+            dot += (long double)h[k] * (long double)fp[k];
+            norm += fabsl((long double)h[k]);
+        }
+        const long double got = (long double)sinc.fms(fp.begin());
+        return fabsl(got - dot) <= 1e-12L * norm;
+    }
+    return true;
+}
+
+template <class Channel, class Sinc>
+std::shared_ptr<const std::vector<double>> probe_taps(const Sinc &sinc) {
+    const int64_t half = (int64_t)sinc.getMo2();
+    if (half < 0 || half > (1 << 24)) throw Error(LCFIR_EINVAL, "sinc.getMo2() out of range");
+    const int64_t T = 2 * half + 1;
+    const Channel fp = fingerprint_window<Channel>(T);
     const double finger = (double)sinc.fms(fp.begin());
     struct Entry {
         int64_t half;
@@ -217,6 +263,25 @@ inline std::string &last_failure() {
     return s;
 }
 
+// The taps of a WindowedSinc-like object as the drop-in sees them: data() /
+// size() when those are consistent with getMo2() / fms() (direct_taps_valid),
+// otherwise recovered through fms() (probe_taps).  For hosts that build an
+// lcfir::Filter themselves (process_buffer_device): c_lib need not expose
+// data() / size().
+template <class Channel, class Sinc>
+std::vector<double> sinc_taps(const Sinc &sinc) {
+    if constexpr (sinc_traits_direct<Sinc>::value) {
+        const double *h = SincTraits<Sinc>::data(sinc);
+        const size_t T = SincTraits<Sinc>::size(sinc);
+        if (detail::direct_taps_valid<Channel>(sinc, h, T)) return std::vector<double>(h, h + T);
+    }
+    if constexpr (sinc_has_fms<Channel, Sinc>::value) {
+        return *detail::probe_taps<Channel>(sinc);
+    } else {
+        throw Error(LCFIR_EINVAL, "sinc exposes neither getMo2()-consistent data()/size() nor fms()");
+    }
+}
+
 // ---- the drop-in ------------------------------------------------------------------
 // Same signature and meaning as FilterCore.h:20-27; any number of threads may
 // call it concurrently on disjoint [startIdx, endIdx) of one channel
@@ -227,11 +292,18 @@ inline void apply_filter_range(const Channel &channel, const Sinc &sinc, Channel
     try {
         std::shared_ptr<Filter> flt;
         if constexpr (sinc_traits_direct<Sinc>::value) {
-            flt = FilterCache::instance().get(SincTraits<Sinc>::data(sinc), SincTraits<Sinc>::size(sinc),
-                                              default_device());
-        } else {
-            const auto taps = detail::probe_taps<Channel>(sinc);
-            flt = FilterCache::instance().get(taps->data(), taps->size(), default_device());
+            const double *h = SincTraits<Sinc>::data(sinc);
+            const size_t T = SincTraits<Sinc>::size(sinc);
+            if (detail::direct_taps_valid<Channel>(sinc, h, T))
+                flt = FilterCache::instance().get(h, T, default_device());
+        }
+        if (!flt) {
+            if constexpr (sinc_has_fms<Channel, Sinc>::value) {
+                const auto taps = detail::probe_taps<Channel>(sinc);
+                flt = FilterCache::instance().get(taps->data(), taps->size(), default_device());
+            } else {
+                throw Error(LCFIR_EINVAL, "sinc exposes neither getMo2()-consistent data()/size() nor fms()");
+            }
         }
         flt->apply_range(detail::in_ptr(channel), (int64_t)std::size(channel), detail::out_ptr(temp_output),
                          (int64_t)startIdx, (int64_t)endIdx, progress);

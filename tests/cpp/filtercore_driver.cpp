@@ -5,7 +5,8 @@
 // variant, writes the raw float32 result and prints "peak <value>".
 //
 // usage: filtercore_driver in.f32 taps.f64 out.f32 nch n threads mode normalize
-//        mode 0 = process_buffer (threaded hand-off), 1 = process_buffer_device
+//        mode 0 = process_buffer (threaded hand-off), 1 = process_buffer_device,
+//        2 / 3 = process_buffer with a PaddedSinc / ReversedSinc
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
@@ -18,6 +19,33 @@ struct WindowedSinc {
     std::vector<double> k;
     const double *data() const { return k.data(); }
     size_t size() const { return k.size(); }
+};
+
+// WindowedSinc stand-ins whose data()/size() are NOT the fms() kernel (c_lib's
+// member layout is unpinned): the drop-in must notice (getMo2() / one fms()
+// fingerprint) and recover the taps through fms() instead.  Padded: two extra
+// zeros at the end; Reversed: the taps back to front.
+struct SincFms {
+    std::vector<double> h;
+    int getMo2() const { return (int)(h.size() - 1) / 2; }
+    template <class It>
+    double fms(It p) const {
+        double acc = 0;
+        for (size_t k = 0; k < h.size(); ++k) acc += h[k] * (double)p[(long)k];
+        return acc;
+    }
+};
+struct PaddedSinc : SincFms {
+    std::vector<double> padded;
+    explicit PaddedSinc(std::vector<double> t) : SincFms{t}, padded(t) { padded.resize(t.size() + 2, 0.0); }
+    const double *data() const { return padded.data(); }
+    size_t size() const { return padded.size(); }
+};
+struct ReversedSinc : SincFms {
+    std::vector<double> rev;
+    explicit ReversedSinc(std::vector<double> t) : SincFms{t}, rev(t.rbegin(), t.rend()) {}
+    const double *data() const { return rev.data(); }
+    size_t size() const { return rev.size(); }
 };
 
 // Counterpart of ThreadSafeProgress (ProgressBar.h:57-82).
@@ -62,9 +90,14 @@ int main(int argc, char **argv) {
         if (mode == 0) {
             peak = lcfir::process_buffer(buf, sinc, opts, &prog);
             if (prog.count != nch * n) { std::fprintf(stderr, "progress %zu\n", prog.count); return 3; }
-        } else {
-            lcfir::Filter flt(sinc.data(), (int32_t)sinc.size());
+        } else if (mode == 1) {
+            const std::vector<double> taps = lcfir::sinc_taps<std::vector<float>>(sinc);
+            lcfir::Filter flt(taps.data(), (int32_t)taps.size());
             peak = lcfir::process_buffer_device(buf, flt, opts);
+        } else if (mode == 2) {
+            peak = lcfir::process_buffer(buf, PaddedSinc(sinc.k), opts, &prog);
+        } else {
+            peak = lcfir::process_buffer(buf, ReversedSinc(sinc.k), opts, &prog);
         }
     } catch (const lcfir::Error &e) {
         std::fprintf(stderr, "lcfir error %d: %s\n", e.code(), e.what());

@@ -88,7 +88,11 @@ def _worker(rank, world, port, nfiles, nch, n, normalize, scope, loud, q):
         r = batch.BatchRunner(OracleBackend(taps), rank, world, [f.shape[1] for f in files], nch,
                               HALF, normalize, scope, allreduce)
         r.prepare(lambda f, lo, hi: files[f][:, lo:hi])
-        r.step()
+        # three steps: with an exchange each step's normalize rides in the next
+        # step's filter launches (BatchRunner defer); results() runs the last
+        # step's pending ones
+        for _ in range(3):
+            r.step()
         q.put((rank, r.exchange, [(sh, y.copy()) for sh, y in r.results()], r.peaks.copy()))
     finally:
         dist.destroy_process_group()
@@ -220,6 +224,59 @@ def test_batch_lanes_pipeline(lanes, normalize):
     assert len(set().union(*outs_by_lane.values())) == nfiles * lanes
     with pytest.raises(ValueError):
         batch.BatchRunner(be, 0, 1, [n], nch, HALF, lanes=0)
+
+
+@pytest.mark.parametrize("lanes,normalize,scope,nfiles", [(1, True, "file", 1), (1, False, "file", 3),
+                                                          (2, True, "file", 2), (3, True, "global", 2)])
+def test_force_exchange_defers_normalize(lanes, normalize, scope, nfiles):
+    """force_exchange at world 1: the all-reduce runs every step (identity
+    here), so BatchRunner defers each shard's normalize into the same shard's
+    filter launch of the lane's next step (two output sets per lane, three peak
+    vectors).  After any number of steps, results() (which runs the pending
+    normalizes) equals the serial reference, and the peaks are each file's."""
+    nch, n = 2, 3000
+    files = make_files(nfiles, nch, n, True)
+    taps = make_taps()
+    calls = []
+
+    class Rec(OracleBackend):
+        inside = False
+
+        def filter_normalize_prev(self, *a, **k):
+            calls.append("fused")
+            self.inside = True  # the CPU stand-in fuses nothing: its own normalize call is not a pass
+            try:
+                return super().filter_normalize_prev(*a, **k)
+            finally:
+                self.inside = False
+
+        def normalize(self, *a, **k):
+            if not self.inside:
+                calls.append("norm")
+            return super().normalize(*a, **k)
+
+    ex = []
+    r = batch.BatchRunner(Rec(taps), 0, 1, [f.shape[1] for f in files], nch, HALF, normalize, scope,
+                          allreduce_max=lambda pk: ex.append(pk.copy()), lanes=lanes, force_exchange=True)
+    assert r.exchange and r.defer and not r.fuse
+    r.prepare(lambda f, lo, hi: files[f][:, lo:hi])
+    ref = reference(nfiles, nch, n, normalize, scope, True)
+    for k in range(2 * lanes + 1):
+        calls.clear()
+        r.step()
+        # a lane's first step has nothing pending; later steps carry one normalize per shard
+        assert calls.count("fused") == (nfiles if k >= lanes else 0) and "norm" not in calls
+        assert len(ex) == k + 1
+    calls.clear()
+    res = r.results()  # flushes the pending normalizes of every lane
+    assert calls.count("norm") == lanes * nfiles
+    for sh, y in res:
+        assert np.array_equal(y, ref[sh.file][:, sh.start:sh.end]), sh.file
+    for k in range(lanes + 1):  # results() after every step: flushed each time
+        r.step()
+        for sh, y in r.results():
+            assert np.array_equal(y, ref[sh.file][:, sh.start:sh.end]), (k, sh.file)
+    r.close()
 
 
 def _preroll_worker(rank, world, port, q):

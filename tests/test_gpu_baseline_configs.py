@@ -228,3 +228,21 @@ def test_configs_4_and_5_batch(tt, oracle_mod):
         else:
             # loud files: config 4 rescaled them already; --normalize gives the same
             assert torch.equal(y, r4.results()[sh.file][1])
+    del r5
+    # config 5's per-rank shape at N = 8: one file per rank with the peak
+    # exchange in every step (force_exchange; the all-reduce is the identity at
+    # world 1, test_gpu_batch.py runs it through RCCL), each step's normalize
+    # carried by the next step's filter launch (BatchRunner defer); results()
+    # runs the last one.  Every sample as the per-file rule gives it.
+    be = batch.DeviceBackend(flt, dev)
+    r = batch.BatchRunner(be, 0, 1, [n], nch, half, True, "file", allreduce_max=lambda t: None,
+                          force_exchange=True)
+    assert r.defer
+    r.prepare(lambda f, lo, hi: src[0][:, lo:hi])
+    for _ in range(3):
+        r.step()
+    (sh, y), = r.results()
+    assert float(r.peaks[0].item()) == peaks4[0]
+    gain = 1.0 / float(np.float32(peaks4[0]))
+    assert torch.equal(y, (pre[0].double() * gain).float())
+    r.close()

@@ -194,9 +194,10 @@ def test_graphed_steps_equal_eager(tt, oracle_mod, lanes, normalize, per_lane):
     be, r = runner()
     g = batch.GraphedSteps(r, be, per_lane=per_lane)
     assert g.per_replay == 2 * lanes and len(g.graphs) == (lanes if per_lane else 1)
-    for outs in r._outs:
-        for y in outs:
-            y.fill_(float("nan"))
+    for sets in r._outs:
+        for outs in sets:
+            for y in outs:
+                y.fill_(float("nan"))
     g.replay()
     torch.cuda.synchronize(dev)
     got = [(sh.file, y.cpu().numpy()) for sh, y in r.results()]
@@ -427,3 +428,106 @@ def test_filter_window_norm_fallbacks(tt, oracle_mod):
     with pytest.raises(lc.LcfirError):  # at least one peak slot
         flt.filter_window_norm_dev(dx, 0, n, n, n, nch, dy, 0, n, 0, n, None, 0, dx, n,
                                    torch.ones(1, device="cuda"), 0, True)
+
+
+@pytest.mark.parametrize("lanes", [1, 3])
+def test_graph_replay_then_eager_steps(tt, oracle_mod, lanes):
+    """GraphedSteps.replay() followed by a number of eager steps that is not a
+    multiple of the replay's step count, with --normalize (every step rescales
+    and clears peak vectors): the lanes' eager steps must queue behind the
+    graph's work on their buffers and the graph behind earlier eager work
+    (one-graph mode launches on lane 0's stream only).  Every output and peak
+    equals an all-eager run of the same step count."""
+    torch, lc = tt
+    import batch
+    import synth
+    taps = oracle_mod.design_lowcut(20.0, 48000.0, 4001)
+    half = (taps.size - 1) // 2
+    files = [synth.file_buffer(1, 200_000 + 1_001 * f, 48000.0, file=f, bits=16) for f in range(2)]
+    files[1] = (files[1] * np.float32(2.0)).astype(np.float32)
+    flt = lc.Filter(taps, method="fft")
+    dev = torch.device("cuda", 0)
+    nf = [f.shape[1] for f in files]
+
+    def fresh():
+        be = batch.DeviceBackend(flt, dev, lanes=lanes, own_streams=True)
+        r = batch.BatchRunner(be, 0, 1, nf, 1, half, True, "file", lanes=lanes)
+        r.prepare(lambda f, lo, hi: files[f][:, lo:hi])
+        return be, r
+
+    be, r = fresh()
+    g = batch.GraphedSteps(r, be)  # one graph for every lane
+    g.replay()
+    extra = g.per_replay // 2 + 1
+    for _ in range(extra):
+        r.step()
+    got = [(sh.file, y.cpu().numpy()) for sh, y in r.results()]
+    got_pk = r.peaks.cpu().numpy()
+    r.close()
+    total = sum(r._steps)  # eager steps the graph stood for are counted at capture
+    be, r = fresh()
+    for _ in range(total):
+        r.step()
+    want = [(sh.file, y.cpu().numpy()) for sh, y in r.results()]
+    assert np.array_equal(r.peaks.cpu().numpy(), got_pk)
+    for (fa, ya), (fb, yb) in zip(want, got):
+        assert fa == fb and np.array_equal(ya, yb), fa
+    r.close()
+    torch.cuda.set_stream(torch.cuda.default_stream(dev))
+
+
+@pytest.fixture(scope="module")
+def nccl_world1(tt):
+    """A world-size-1 RCCL process group on this GPU (torch.distributed
+    backend "nccl" is RCCL on ROCm): BatchRunner(force_exchange=True) then
+    runs the config-5 peak all-reduce through RCCL on the lane streams."""
+    torch, _ = tt
+    import socket
+    import torch.distributed as dist
+    if dist.is_initialized():
+        pytest.skip("a process group already exists")
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
+    yield dist
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("lanes,normalize", [(1, True), (2, True), (1, False)])
+def test_rccl_peak_exchange_world1(tt, oracle_mod, nccl_world1, lanes, normalize):
+    """The RCCL leg on the device: torch_allreduce_max (ncclAllReduce MAX of
+    the [num_files] peak vector) on the lane streams every step, with each
+    file's normalize deferred into the next step's filter launch (BatchRunner
+    defer).  Outputs and peaks are bit-identical to the no-exchange run
+    (normalize fused within the step), over several steps, and the output
+    matches ProcessFile.cp:91-101 against the oracle."""
+    torch, lc = tt
+    import batch
+    import synth
+    taps = oracle_mod.design_lowcut(20.0, 48000.0, 4001)
+    half = (taps.size - 1) // 2
+    files = [synth.file_buffer(2, 150_001 + 9_999 * f, 48000.0, file=f, bits=24) for f in range(3)]
+    files[2] = (files[2] * np.float32(3.0)).astype(np.float32)
+    flt = lc.Filter(taps, method="fft")
+    dev = torch.device("cuda", 0)
+    res = []
+    for exchange in (False, True):
+        be = batch.DeviceBackend(flt, dev, lanes=lanes)
+        r = batch.BatchRunner(be, 0, 1, [f.shape[1] for f in files], 2, half, normalize, "file",
+                              batch.torch_allreduce_max(), lanes=lanes, force_exchange=exchange)
+        assert r.exchange == exchange and r.defer == exchange
+        r.prepare(lambda f, lo, hi: files[f][:, lo:hi])
+        for _ in range(2 * lanes + 1):
+            r.step()
+        res.append(([(sh.file, y.cpu().numpy()) for sh, y in r.results()], r.peaks.cpu().numpy()))
+        r.close()
+    (ya, pa), (yb, pb) = res
+    assert np.array_equal(pa, pb)
+    for (fa, a), (fb, b) in zip(ya, yb):
+        assert fa == fb and np.array_equal(a, b), fa
+    for f, y in ya:
+        ref = files[f].copy()
+        oracle_mod.process_buffer(ref, taps, nthreads=1, normalize=normalize, mode=oracle_mod.MODE_LD)
+        assert _ulps(y, ref).max() <= 1, f

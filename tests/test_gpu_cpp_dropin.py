@@ -34,12 +34,19 @@ def run(driver, tmp_path, x, taps, threads, mode, normalize):
 
 
 @pytest.mark.parametrize("threads,mode,normalize", [(1, 0, False), (4, 0, False), (7, 0, True),
-                                                    (1, 1, False), (1, 1, True)])
+                                                    (1, 1, False), (1, 1, True), (3, 2, False),
+                                                    (3, 3, False)])
 def test_cpp_process_buffer(driver, tmp_path, oracle_mod, threads, mode, normalize):
+    """Modes 2 and 3: a sinc whose data()/size() are not the fms() kernel
+    (padded / reversed; the random_int24 taps are asymmetric) -- the drop-in
+    must fall back to recovering the taps through fms()."""
     g = load_golden("random_int24")
-    y, peak = run(driver, tmp_path, g["x"], g["taps"], threads, mode, normalize)
+    taps = g["taps"]
+    if mode == 3:  # visibly asymmetric, so reversed taps filter differently
+        taps = taps + 1e-3 * np.linspace(-1.0, 1.0, taps.size)
+    y, peak = run(driver, tmp_path, g["x"], taps, threads, mode, normalize)
     ref = g["x"].copy()
-    ref_peak = oracle_mod.process_buffer(ref, g["taps"], nthreads=2, normalize=normalize,
+    ref_peak = oracle_mod.process_buffer(ref, taps, nthreads=2, normalize=normalize,
                                          mode=oracle_mod.MODE_LD)
     d = y.astype(np.float64) - ref
     assert np.sqrt(np.mean(d * d)) <= 1e-9

@@ -284,3 +284,39 @@ def test_cli_random_batch(tmp_path, oracle_mod, seed):
             tol = lsb * 1.000001 + np.spacing(np.abs(want_f).astype(np.float32)).astype(np.float64)
             assert np.all(diff <= tol), p.name
             assert np.sum(diff > 0) <= max(2, 1e-4 * diff.size), p.name
+
+
+def test_batch_over_device_stages(tmp_path, oracle_mod):
+    """--devices: a batch dealt round-robin over GPU stages (north_star: one
+    file per GPU).  On the one-GPU box the stages share device 0 ("0,0,0":
+    three stages, each with its own contexts, streams and slots): every output
+    byte-identical to the single-stage run, written in input order, checked
+    against the oracle; with a missing input in the middle the files before it
+    are written and the ones after it are not (main.cp:131-146)."""
+    specs = [(48000, 2, "s24le", "wav", 60000), (44100, 1, "s16le", "wav", 20001),
+             (96000, 2, "f32le", "wav", 40000), (48000, 1, "s24be", "aif", 33333),
+             (48000, 3, "s32le", "wav", 25000), (44100, 2, "s16be", "aif", 12345),
+             (48000, 2, "s24le", "wav", 50001)]
+    srcs = []
+    for i, (rate, nch, fmt, ext, n) in enumerate(specs):
+        x = tone(nch, n, rate, amp=0.9 if i == 4 else 0.4)
+        p = tmp_path / f"d{i}.{ext}"
+        (pcm_ref.write_wave if ext == "wav" else pcm_ref.write_aiff)(p, x, rate, fmt)
+        srcs.append((p, x, rate, fmt))
+    one, three = tmp_path / "one", tmp_path / "three"
+    lowcut("-n", "-f", 25, "-s", 50, "--devices", "0", *[s[0] for s in srcs], one)
+    out = lowcut("-n", "-f", 25, "-s", 50, "--devices", "0,0,0", "--timing", *[s[0] for s in srcs], three)
+    names = [line.split(": ", 1)[1] for line in out.splitlines() if line.startswith("Processing file:")]
+    assert names == [s[0].name for s in srcs]
+    assert "3 GPU stage(s)" in out
+    for p, x, rate, fmt in srcs:
+        assert open(one / p.name, "rb").read() == open(three / p.name, "rb").read(), p.name
+        xq = pcm_ref.np_decode(pcm_ref.np_encode(x, fmt), fmt, x.shape[0])
+        check_file(oracle_mod, p, three / p.name, xq, rate, fmt, 25, 50, True)
+    stop = tmp_path / "stop"
+    args = ["-f", 20, "-s", 48, "--devices", "0,0", *[s[0] for s in srcs[:3]], tmp_path / "missing.wav",
+            *[s[0] for s in srcs[3:]], stop]
+    r = subprocess.run([LOWCUT, *map(str, args)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 1 and "not found" in r.stderr
+    assert all((stop / s[0].name).exists() for s in srcs[:3])
+    assert not any((stop / s[0].name).exists() for s in srcs[3:])

@@ -430,46 +430,22 @@ def gpu_filter_window(lc, flt, x, start, end, x_lo, x_hi):
     return y
 
 
-_CHUNK_CHILD = """
-import sys, numpy as np
-sys.path[:0] = [{pkg!r}, {oracle!r}]
-import lcfir, synth
-x = synth.file_buffer(1, {n}, 48000.0, file=6, bits=24)
-taps = np.load({taps!r})
-flt = lcfir.Filter(taps, method="fft")
-dx = lcfir.DeviceBuffer.from_array(x); dy = lcfir.DeviceBuffer(x.nbytes); dpk = lcfir.DeviceBuffer(4)
-lcfir.peak_reset_dev(dpk, 1)
-flt.filter_channels_dev(dx, {n}, 1, {n}, dy, {n}, dpk)
-lcfir.sync()
-np.savez({out!r}, y=dy.download((1, {n})), pk=dpk.download(1))
-"""
-
-
-def test_fft_partitioned_chunk_seams(lc, oracle_mod, tmp_path):
+def test_fft_partitioned_chunk_seams(lc, oracle_mod):
     """A partitioned filter with launches split into 65 536-output chunks
-    (LCFIR_FFT_CHUNK, read once per process, so in a child process): the f64
-    partial-sum scratch restarts at every seam.  Checked around each seam."""
-    import os
-    import subprocess
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    (lcfir_ctx_set_fft_tuning chunk): the f64 partial-sum scratch restarts at
+    every seam.  Bit-identical to the unchunked launch, and checked around each
+    seam against the long-double oracle."""
+    import synth
     n, chunk = 400_000, 65_536
     taps = oracle_mod.design_lowcut(20.0, 48000.0, 19201)
-    np.save(tmp_path / "taps.npy", taps)
-    code = _CHUNK_CHILD.format(pkg=os.path.join(root, "audio-fir-filter_amd"),
-                               oracle=os.path.join(root, "oracle"), n=n,
-                               taps=str(tmp_path / "taps.npy"), out=str(tmp_path / "y.npz"))
-    env = dict(os.environ, LCFIR_FFT_CHUNK=str(chunk))
-    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
-                       timeout=600)
-    assert r.returncode == 0, r.stderr[-2000:]
-    d = np.load(tmp_path / "y.npz")
-    y, pk = d["y"][0], d["pk"][0]
-    import synth
-    x = synth.file_buffer(1, n, 48000.0, file=6, bits=24)[0]
+    x = synth.file_buffer(1, n, 48000.0, file=6, bits=24)
+    y_one, pk_one = gpu_filter_channels(lc, lc.Filter(taps, method="fft"), x)
+    flt = lc.Filter(taps, method="fft")
+    flt.set_fft_tuning(chunk=chunk)
+    y, pk = gpu_filter_channels(lc, flt, x)
+    y, pk, x = y[0], pk[0], x[0]
     # chunks are whole segments of the channel's grid: the unchunked launch
-    # (this process) gives the same bytes
-    y_one, pk_one = gpu_filter_channels(lc, lc.Filter(taps, method="fft"), x[None, :])
+    # gives the same bytes
     assert np.array_equal(y, y_one[0]) and pk == pk_one[0]
     seams = np.r_[[s + o for s in range(chunk, n, chunk) for o in range(-3, 3)]]
     idx = np.unique(np.r_[_sample_positions(n, 9600, 512, 61), seams])
@@ -479,84 +455,35 @@ def test_fft_partitioned_chunk_seams(lc, oracle_mod, tmp_path):
     assert pk == np.abs(y).max()
 
 
-_GROUP_CHILD = """
-import sys, numpy as np
-sys.path[:0] = [{pkg!r}, {oracle!r}]
-import lcfir, synth
-nch, n = 5, {n}
-x = synth.file_buffer(nch, n, 48000.0, file=8, bits=24)
-out = {{}}
-for name in ("sym", "part"):
-    flt = lcfir.Filter(np.load({taps!r}.replace("NAME", name)), method="fft")
-    dx = lcfir.DeviceBuffer.from_array(x); dy = lcfir.DeviceBuffer(x.nbytes)
-    pk = lcfir.DeviceBuffer.from_array(np.zeros(nch, np.float32))
-    flt.filter_channels_dev(dx, n, nch, n, dy, n, pk)
-    lcfir.sync()
-    out["y_" + name] = dy.download((nch, n))
-    out["pk_" + name] = pk.download((nch,), np.float32)
-np.savez({out!r}, **out)
-"""
-
-
 @pytest.mark.parametrize("max_units", [7, 20])
-def test_fft_channel_groups(tmp_path, max_units):
+def test_fft_channel_groups(lc, max_units):
     """The kernels index units in 32 bits, so fft_launch splits a launch into
-    channel groups of at most 2^31 - 1 units (fir_fft.hpp FftGrid).
-    LCFIR_FFT_MAX_UNITS (read once per process: child processes) forces the
-    split at small sizes -- one channel per launch (7) and groups of two (20,
-    9 segments per channel) -- for a zero-phase and a partitioned filter, with
-    per-channel peaks: every output and peak bit-identical to one launch."""
-    import os
-    import subprocess
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    import lcfir
-    np.save(tmp_path / "sym.npy", lcfir.design_lowcut(20.0, 4.0, 48000.0))
-    np.save(tmp_path / "part.npy", lcfir.design_lowcut(20.0, 10.0, 48000.0))
-    res = {}
-    for mu in (None, max_units):
-        out = tmp_path / f"y_{mu}.npz"
-        code = _GROUP_CHILD.format(pkg=os.path.join(root, "audio-fir-filter_amd"),
-                                   oracle=os.path.join(root, "oracle"), n=100_000,
-                                   taps=str(tmp_path / "NAME.npy"), out=str(out))
-        env = dict(os.environ)
-        env.pop("LCFIR_FFT_MAX_UNITS", None)
-        if mu:
-            env["LCFIR_FFT_MAX_UNITS"] = str(mu)
-        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
-                           timeout=600)
-        assert r.returncode == 0, r.stderr[-2000:]
-        res[mu] = np.load(out)
-    for k in res[None].files:
-        assert np.array_equal(res[None][k], res[max_units][k]), k
-    assert np.all(res[None]["pk_sym"] > 0)
+    channel groups of at most 2^31 - 1 units (fir_fft.hpp FftGrid).  The
+    max_units tuning forces the split at small sizes -- one channel per launch
+    (7) and groups of two (20, 9 segments per channel) -- for a zero-phase and
+    a partitioned filter, with per-channel peaks: every output and peak
+    bit-identical to one launch."""
+    import synth
+    nch, n = 5, 100_000
+    x = synth.file_buffer(nch, n, 48000.0, file=8, bits=24)
+    for taps in (lc.design_lowcut(20.0, 4.0, 48000.0), lc.design_lowcut(20.0, 10.0, 48000.0)):
+        y0, pk0 = gpu_filter_channels(lc, lc.Filter(taps, method="fft"), x)
+        flt = lc.Filter(taps, method="fft")
+        flt.set_fft_tuning(max_units=max_units)
+        y1, pk1 = gpu_filter_channels(lc, flt, x)
+        assert np.array_equal(y0, y1) and np.array_equal(pk0, pk1)
+        assert np.all(pk0 > 0)
 
 
 # ---- linear-phase filters: the zero-phase form (fir_fft.hpp fft_sym_eligible)
-_SYM_CHILD = """
-import sys, numpy as np
-sys.path[:0] = [{pkg!r}, {oracle!r}]
-import lcfir, synth
-x = synth.file_buffer(2, {n}, 48000.0, file=7, bits=24)
-flt = lcfir.Filter(np.load({taps!r}), method="fft")
-dx = lcfir.DeviceBuffer.from_array(x); dy = lcfir.DeviceBuffer(x.nbytes)
-flt.filter_channels_dev(dx, {n}, 2, {n}, dy, {n}, None)
-lcfir.sync()
-np.save({out!r}, dy.download((2, {n})))
-"""
-
-
 @pytest.mark.parametrize("ntaps,perturb", [(4001, 0.0), (4001, 1e-9), (4003, 0.0), (801, 0.0)])
-def test_fft_zero_phase_form(lc, oracle_mod, tmp_path, ntaps, perturb):
+def test_fft_zero_phase_form(lc, oracle_mod, ntaps, perturb):
     """Symmetric taps with an even half run in zero-phase form (real pair
     table, outputs c in [half, L - half)); odd halves and taps with a visible
     antisymmetric part run the general table.  Every form against the
     long-double oracle, sub-ranges against whole channels (the shifted output
-    window), and the zero-phase form against the general one run in a child
-    process with LCFIR_FFT_SYM=0."""
-    import os
-    import subprocess
-    import sys
+    window), and the zero-phase form against the general one on the same
+    filter (lcfir_ctx_set_fft_tuning zero_phase 0)."""
     import synth
     fs, n = 48000.0, 200_003
     taps = oracle_mod.design_lowcut(20.0, fs, ntaps)
@@ -573,12 +500,37 @@ def test_fft_zero_phase_form(lc, oracle_mod, tmp_path, ntaps, perturb):
         assert max_ulps(y[c][idx], ref_ld) <= 1
     for start, end in [(1, n - 1), (half - 1, half + 12_385), (77_777, 77_778), (n - 13_000, n)]:
         check_window(lc, flt, x, y, start, end)
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    np.save(tmp_path / "taps.npy", taps)
-    code = _SYM_CHILD.format(pkg=os.path.join(root, "audio-fir-filter_amd"), oracle=os.path.join(root, "oracle"),
-                             n=n, taps=str(tmp_path / "taps.npy"), out=str(tmp_path / "y.npy"))
-    env = dict(os.environ, LCFIR_FFT_SYM="0")
-    subprocess.run([sys.executable, "-c", code], check=True, env=env, timeout=300)
-    y_general = np.load(tmp_path / "y.npy")
+    # the general pair table on the same filter (zero-phase form off)
+    assert flt.fft_info["zero_phase"] == (perturb == 0.0 and ((ntaps - 1) // 2) % 2 == 0)
+    flt_g = lc.Filter(taps, method="fft")
+    flt_g.set_fft_tuning(zero_phase=False)
+    y_general, _ = gpu_filter_channels(lc, flt_g, x)
+    assert not flt_g.fft_info["zero_phase"]
     assert max_ulps(y, y_general) <= 1
     assert rms(y, y_general) <= RMS_TOL
+
+
+def test_staging_pool_cap_release_and_ctx_destroy(lc, oracle_mod):
+    """lcfir_apply_range's staging pool: 40 concurrent range calls on one
+    channel share at most 16 slots (the rest wait for one), the result is the
+    one-range bytes; lcfir_staging_release frees every idle slot and its
+    stream, later calls make new ones, and destroying the ctx afterwards does
+    not touch the released streams (apply_range never registers them with the
+    ctx).  A partitioned filter, so the ctx also kept per-stream scratch."""
+    g = load_golden("random_int24")
+    x = np.ascontiguousarray(g["x"][0], np.float32)
+    taps = oracle_mod.design_lowcut(20.0, 48000.0, 19201)
+    flt = lc.Filter(taps, method="fft")
+    whole = np.zeros_like(x)
+    flt.apply_range(x, whole, 0, x.size)
+    y = lc.filter_channel(x, flt, 40)
+    assert np.array_equal(y, whole)
+    live, idle = lc.staging_count(0)
+    assert 1 <= live <= 16 and idle == live
+    lc.staging_release(0)
+    assert lc.staging_count(0) == (0, 0)
+    assert np.array_equal(lc.filter_channel(x, flt, 5), whole)
+    lc.staging_release(-1)
+    flt.close()
+    ref = oracle_mod.filter_channel(x, taps, oracle_mod.MODE_LD)
+    assert rms(whole, ref) <= RMS_TOL and max_ulps(whole, ref) <= 1

@@ -124,3 +124,31 @@ def test_truncated_ssnd_header(tmp_path, ssnd_body):
     p.write_bytes(b"FORM" + struct.pack(">I", 4 + len(body)) + b"AIFF" + body)
     r = run("--info", p)
     assert r.returncode == 1 and "SSND" in r.stderr
+
+
+def test_plan_deals_files_round_robin(tmp_path):
+    """--plan prints the batch's dealing without touching a GPU: file i goes to
+    stage i mod D of the --devices list (north_star: one file per GPU)."""
+    files = []
+    for i in range(7):
+        p = tmp_path / f"p{i}.wav"
+        pcm_ref.write_wave(p, sig(1, 100, i), 48000, "s16le")
+        files.append(p)
+    outdir = tmp_path / "o"
+    for devs in ("0,1,2", "3,1", "0,0", "5"):
+        r = run("--plan", "--devices", devs, *files, outdir)
+        assert r.returncode == 0, r.stderr
+        d = [int(v) for v in devs.split(",")]
+        lines = r.stdout.strip().splitlines()
+        assert len(lines) == len(files)
+        for i, line in enumerate(lines):
+            f = line.split()
+            assert f[1] == str(files[i]) and f[3] == str(outdir / files[i].name)
+            assert int(f[5]) == i % len(d) and int(f[7]) == d[i % len(d)]
+    r = run("--plan", "--device", "2", files[0], tmp_path / "single.wav")
+    assert r.returncode == 0 and r.stdout.split()[-1] == "2"
+    for bad in ("0,,1", "x", "1,-2"):
+        r = run("--plan", "--devices", bad, *files, outdir)
+        assert r.returncode == 1 and "--devices" in r.stderr
+    r = run("--plan", *files, outdir)
+    assert r.returncode == 1 and "--plan needs --devices" in r.stderr
