@@ -48,6 +48,7 @@ struct DirectParams {
     int64_t peak_stride;
     double *y64;        // partitioned FFT only: f64 partial sums, element 0 = output `start`
     int64_t y64_stride;
+    double2 *park;      // L = 32768 FFT only: the workgroups' park slabs (fir_fft32.hpp)
 };
 
 template <int R>

@@ -126,6 +126,7 @@ constexpr size_t kFftPairTable = (size_t)3 * kFftPairSlots * kFftNT; // double2 
 // The defaults are the product's; tests set the others explicitly (no
 // environment variable is read anywhere in the library).
 struct FftTuning {
+    int32_t seg_len = 0;    // segment length in real samples: 0 = by tap count (fft_choose_seg_len), 16384, 32768
     int32_t zero_phase = 1; // 1: linear-phase filters run in zero-phase form (fft_sym_eligible); 0: general table
     int64_t chunk = 0;      // outputs per launch chunk; 0 = 2^28 (the buffer offsets' 32-bit range)
     int64_t max_units = 0;  // units per launch; 0 = 2^31 - 1 (FftGrid's 32-bit unit index)
@@ -137,13 +138,14 @@ struct FftTuning {
 // f64 (fir_fft_f64_kernel's output modes).
 struct FftPlan {
     bool ready = false;
+    int L = 16384;             // segment length (real samples): fir_fft_f64_kernel or, 32768, fir_fft32_f64_kernel
     int ntaps = 0;             // taps per partition (the filter's own count when parts == 1)
     int parts = 1;
     int B = 0;                 // outputs per segment = L - ntaps + 1
-    double2 *d_pair = nullptr; // parts x [3][kFftPairSlots][512]: 2S, 2D, W_L^k per (slot, thread)
+    double2 *d_pair = nullptr; // parts x halves x [3][kFftPairSlots][512]: 2S, 2D, W_L^k per (slot, thread)
     std::vector<double2> c8;   // per partition: the special lane's bin-M/2 coefficient
-    double2 *d_tw = nullptr;   // kFftTw twiddles
-    uint32_t *d_task = nullptr; // [512] task words (cA, d1A, e1A, cB, d1B, e1B)
+    double2 *d_tw = nullptr;   // kFftTw twiddles (kFft32Tw for L = 32768)
+    uint32_t *d_task = nullptr; // [halves][512] task words (cA, d1A, e1A, cB, d1B, e1B)
     int cus = 256;             // compute units of the plan's device (persistent grid)
     bool sym = false;          // linear-phase filter run in zero-phase form (kFftOutSym)
     FftTuning tune;            // the ctx's tuning when the plan was built
@@ -175,21 +177,35 @@ inline int fft_partition_taps(int ntaps, int parts) {
     const int t = (ntaps + parts - 1) / parts;
     return t | 1;
 }
-// partition count minimising the work per output, parts / (L - taps + 1)
-inline int fft_partition_count(int ntaps) {
+// partition count minimising the work per output, parts / (L - taps + 1), for
+// segments of L real samples (a partition keeps at least kFftMinB outputs)
+inline int fft_partition_count(int ntaps, int L = 16384) {
     int best = 0;
     double best_cost = 0.0;
     for (int n = 1; n <= ntaps; ++n) {
         const int t = fft_partition_taps(ntaps, n);
-        if (t > kFftMaxPartTaps) continue;
-        const double cost = (double)n / (double)(kFftL - t + 1);
+        if (t > L - kFftMinB + 1) continue;
+        const double cost = (double)n / (double)(L - t + 1);
         if (best == 0 || cost < best_cost) {
             best = n;
             best_cost = cost;
         }
-        if (t < kFftL / 4) break; // more partitions only add launches from here
+        if (t < L / 4) break; // more partitions only add launches from here
     }
     return best;
+}
+// Relative cost of one L = 32 768 segment (fir_fft32.hpp: two 8192-point
+// halves plus the radix-2 split and merge) against one L = 16 384 segment:
+// f64 instructions per thread, 3 348 against 1 470.
+constexpr double kFft32SegCost = 2.28;
+// Segment length for a filter: the one with the lower estimated work per
+// output, cost(L) x parts / (L - taps + 1); the longer segment only when it
+// saves at least 5 % (the L = 16 384 kernel also carries a fused normalize).
+inline int fft_choose_seg_len(int ntaps) {
+    const int p16 = fft_partition_count(ntaps, 16384), p32 = fft_partition_count(ntaps, 32768);
+    const double c16 = (double)p16 / (double)(16384 - fft_partition_taps(ntaps, p16) + 1);
+    const double c32 = kFft32SegCost * p32 / (double)(32768 - fft_partition_taps(ntaps, p32) + 1);
+    return c32 < 0.95 * c16 ? 32768 : 16384;
 }
 
 // LDS slot of column c: a wave's two columns sit in adjacent 8 KiB blocks
@@ -484,22 +500,25 @@ __device__ __forceinline__ int fx4(int d1, int b0, int g0) {
 // loaded window [x_lo, x_hi): offsets outside it -- including "negative" ones,
 // which wrap to huge unsigned offsets -- read 0.  That is the zero padding of
 // FilterCore.h's shortened edge sums, with no branches.
+// NR float2 per thread: 16 for L = 16 384, 32 for fir_fft32.hpp's L = 32 768.
+template <int NR>
 __device__ __forceinline__ void fft_load_unit(const DirectParams &p, int ch, int64_t n0, int j,
-                                              float2 (&v)[16]) {
+                                              float2 (&v)[NR]) {
+    constexpr int kSeg = 1024 * NR; // real samples per segment
     const float *x = p.x + (int64_t)ch * p.x_stride;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float *>(x), (short)0, (int)((p.x_hi - p.x_lo) * 4), 0x00020000);
     const int64_t w0 = n0 - p.half - p.x_lo; // window start inside the loaded range
     const int off0 = (int)(w0 * 4) + 8 * j;   // may be negative
-    if (w0 >= 0 && w0 + kFftL <= p.x_hi - p.x_lo) {
+    if (w0 >= 0 && w0 + kSeg <= p.x_hi - p.x_lo) {
         // interior unit (all but the first and last of a range): cached
         // dwordx2 loads (4-byte aligned is enough for buffer loads)
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
+        for (int r = 0; r < NR; ++r)
             v[r] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rsrc, off0 + 8 * 512 * r, 0, 0));
     } else {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
+        for (int r = 0; r < NR; ++r) {
             const int off = off0 + 8 * 512 * r;
             // aux bit 31 = volatile: keeps the two dword loads from being merged
             // into one dwordx2, whose range check is all-or-nothing (a pair
@@ -670,6 +689,225 @@ __device__ __forceinline__ void fft_nrm_store(const FftNrm &nrm, int u, int t, d
         nrm.y[tail + t] = (float)((double)nrm.y[tail + t] * gain);
 }
 
+// Column phase of one 8192-point transform held in the LDS work array
+// (DESIGN.md s4.2): wave w owns the two columns in LDS slots 2w and 2w + 1 and
+// runs their 512-point DFTs as 8 x 8 x 8 with wave-local exchanges (stages A,
+// B), stage C per task, the pair step in registers, then the inverse stages
+// A', B', C' back into the same slots.  LDS in, LDS out: the workgroup
+// barriers around it are the caller's.  tk_all: this thread's task word;
+// pair: the pair table of this transform; c8: the special lane's bin-M/2
+// coefficient.  odd (wave-uniform): the transform has no self-paired bins
+// (fir_fft32.hpp half O: columns w and 15 - w in every wave, task B the
+// mirror of task A), so wave 0 runs the generic pair loop.  after_pair() runs
+// between the pair step and stage A' (the caller's prefetch, or nothing).
+// kReuseTw: the zero-phase form keeps stage A's and B's twiddle powers for A'
+// and B' (56 VGPRs across the pair step; off where the caller parks data).
+template <int kOut, bool kReuseTw = true, class AfterPair>
+__device__ __forceinline__ void fft_columns(double2 *flds, const double2 *twl, const double2 *__restrict__ pair,
+                                            uint32_t tk_all, double2 c8, bool odd, int j, int rnd,
+                                            AfterPair &&after_pair) {
+    (void)rnd; // phase stamps only (LCFIR_FFT_TRACE)
+    const int lane = j & 63;
+    const int w = j >> 6;
+    // the wave's two columns in adjacent slots
+    double2 *blk0 = flds + 512 * (2 * w);
+    double2 *blk1 = blk0 + 512;
+    double2 x0[8], x1[8]; // the wave's two columns (later: tasks A and B)
+    double2 tws[8];
+    // Stages A and B run as a two-column software pipeline: a column's
+    // exchange reads are issued right behind its writes, and the other
+    // column's arithmetic covers their latency (counted lgkmcnt waits).
+    // ---- stage A: lane l holds b = l + 64 t; radix-8 over t -> d1; * W_512^(l d1)
+    const int l1 = lane & 7, d1s = lane >> 3; // the stage-B lane (l1, d1)
+#pragma unroll
+    for (int t = 0; t < 8; ++t) x0[t] = blk0[lane + 64 * t];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) x1[t] = blk1[lane + 64 * t];
+    powers8(twl[512 + lane], tws);
+    double2 tws_a[8]; // W_512^(lane r): stage A' of task A needs the same powers (waves 1..7, wave 0 lanes < 32)
+    if constexpr (kOut == kFftOutSym && kReuseTw) {
+#pragma unroll
+        for (int r = 1; r < 8; ++r) tws_a[r] = tws[r];
+    }
+    dft8(x0);
+    twiddle8(x0, tws);
+#pragma unroll
+    for (int d1 = 0; d1 < 8; ++d1) blk0[fx1(lane, d1)] = x0[d1];
+    wave_lds_sync();
+#pragma unroll
+    for (int l2 = 0; l2 < 8; ++l2) x0[l2] = blk0[fx1(l1 + 8 * l2, d1s)];
+    __builtin_amdgcn_sched_barrier(0);
+    dft8(x1);
+    twiddle8(x1, tws);
+#pragma unroll
+    for (int d1 = 0; d1 < 8; ++d1) blk1[fx1(lane, d1)] = x1[d1];
+    wave_lds_sync();
+#pragma unroll
+    for (int l2 = 0; l2 < 8; ++l2) x1[l2] = blk1[fx1(l1 + 8 * l2, d1s)];
+    __builtin_amdgcn_sched_barrier(0);
+    FFT_STAMP(5);
+    // ---- stage B: lane (l1, d1) has gathered l2; radix-8 -> e1; * W_64^(l1 e1)
+    powers8(twl[512 + 8 * l1], tws);
+    double2 tws_b[8]; // W_64^(l1 r): stage B' (d1 = lane & 7 = l1) needs the same powers
+    if constexpr (kOut == kFftOutSym && kReuseTw) {
+#pragma unroll
+        for (int r = 1; r < 8; ++r) tws_b[r] = tws[r];
+    }
+    dft8(x0);
+    twiddle8(x0, tws);
+#pragma unroll
+    for (int e1 = 0; e1 < 8; ++e1) blk0[fx2(l1, d1s, e1)] = x0[e1];
+    __builtin_amdgcn_sched_barrier(0);
+    dft8(x1);
+    twiddle8(x1, tws);
+#pragma unroll
+    for (int e1 = 0; e1 < 8; ++e1) blk1[fx2(l1, d1s, e1)] = x1[e1];
+    wave_lds_sync();
+    FFT_STAMP(6);
+    // ---- pair-table loads, issued ahead of stage C (L2 latency off the path)
+    constexpr bool kSym = kOut == kFftOutSym;
+    double2 qs[kSym ? 1 : 8], qd[kSym ? 1 : 8]; // 2 S and 2 D of the pair in slot i
+    double2 qpq[kSym ? 8 : 1], qp2[kSym ? 4 : 1]; // kSym: (p1, q2) of slot i, p2 of slots 2m, 2m+1
+    double2 wbase;                                // W_L^k of slot 0 (general form)
+    if constexpr (kSym) {
+        const double2 *t = pair + j;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) qpq[i] = t[kFftSymPQ + 512 * i]; // one 16-byte load per slot
+#pragma unroll
+        for (int m = 0; m < 4; ++m) qp2[m] = t[kFftSymP2 + 512 * m];
+    } else {
+        const double2 *t = pair + j;
+        wbase = pair[2 * kFftPairSlots * 512 + j];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            qs[i] = t[512 * i];
+            qd[i] = t[kFftPairSlots * 512 + 512 * i];
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0); // keep the loads ahead of stage C
+    // ---- stage C: per task, radix-8 over l1 -> e2: x0[e2] = X[kA], x1[e2] = X[kB]
+    const uint32_t tk = tk_all;
+    const int cA = tk & 15, dA = (tk >> 4) & 7, eA = (tk >> 7) & 7; // cA, cB: LDS slots
+    const int cB = (tk >> 10) & 15, dB = (tk >> 14) & 7, eB = (tk >> 17) & 7;
+    {
+        const double2 *ba = flds + 512 * cA, *bb = flds + 512 * cB;
+#pragma unroll
+        for (int l1 = 0; l1 < 8; ++l1) x0[l1] = ba[fx2(l1, dA, eA)];
+#pragma unroll
+        for (int l1 = 0; l1 < 8; ++l1) x1[l1] = bb[fx2(l1, dB, eB)];
+    }
+    dft8(x0);
+    dft8(x1);
+    FFT_STAMP(7);
+    // ---- pair step in registers: pairs (x0[i], x1[7-i]); outputs conj(V).
+    // The real split, the multiply by G and the merge collapse to
+    //   conj(V_k) = conj(Z_k P1 + conj(Z_{M-k}) P2),  conj(V_{M-k}) = conj(Z_{M-k}) Q2 - Z_k P2
+    // with S = G_k + conj(G_{M-k}), D = G_k - conj(G_{M-k}), W = W_L^k:
+    //   P1 = 2 (S + D Im W),  P2 = 2i D Re W,  Q2 = 2 (S - D Im W)
+    // General form: the table holds 2S and 2D per (slot, thread) (host, long
+    // double) and W comes from one per-thread base times W_16^i.  Zero-phase
+    // form: the table holds P1 = p1, Q2 = q2 and P2 / i = p2 per bin.
+    {
+        // Wave 0 (a scalar, wave-uniform branch) permutes its special lane
+        // into the generic layout first (fft_w0_permute_in).
+        const bool w0 = !odd && __builtin_amdgcn_readfirstlane(w) == 0;
+        const bool sp = w0 && lane == kFftSpecialLane;
+        double2 wb_hi = wbase; // W base of slots 4..7 (general form; the zero-phase table has per-bin p1, q2, p2)
+        double2 v4 = x1[4];    // special lane: B_4, bin M/2 (slot 8, W = -i): P1 = 2S - 2D, P2 = 0
+        if (w0) {
+            v4 = cconj(cmul(v4, c8)); // a kernel argument (SGPRs: no L2 wait here)
+            if constexpr (!kSym) wb_hi = csel(sp, make_double2(0.0, 1.0), wbase);
+            fft_w0_permute_in(x0, x1, sp);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            if constexpr (kSym)
+                fft_pair_sym(x0[i], x1[7 - i], qpq[i].x, qpq[i].y, (i & 1) ? qp2[i >> 1].y : qp2[i >> 1].x, x0[i],
+                             x1[7 - i]);
+            else
+                fft_pair(x0[i], x1[7 - i], fft_pair_w(i < 4 ? wbase : wb_hi, i), qs[i], qd[i], x0[i],
+                         x1[7 - i]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (w0) fft_w0_permute_out(x0, x1, sp, v4);
+    }
+
+    FFT_STAMP(8);
+    after_pair(); // the caller's prefetch of the next unit's samples
+
+    // ---- inverse stage A': per task radix-8 over e2 -> beta0; * W_512^(beta0 d')
+    {
+        double2 *ba = flds + 512 * cA, *bb = flds + 512 * cB;
+        if constexpr (kOut == kFftOutSym && kReuseTw) {
+            // task A's d' = dA + 8 eA is the lane except in wave 0's column-0
+            // lanes (kFftWave0C0) of an even transform: a wave-uniform choice
+            if (odd || __builtin_amdgcn_readfirstlane(w) != 0) {
+#pragma unroll
+                for (int r = 1; r < 8; ++r) tws[r] = tws_a[r];
+            } else {
+                powers8(twl[512 + dA + 8 * eA], tws);
+            }
+        } else {
+            powers8(twl[512 + dA + 8 * eA], tws);
+        }
+        dft8(x0);
+        twiddle8(x0, tws);
+#pragma unroll
+        for (int b0 = 0; b0 < 8; ++b0) ba[fx3(dA, eA, b0)] = x0[b0];
+        __builtin_amdgcn_sched_barrier(0);
+        powers8(twl[512 + dB + 8 * eB], tws);
+        dft8(x1);
+        twiddle8(x1, tws);
+#pragma unroll
+        for (int b0 = 0; b0 < 8; ++b0) bb[fx3(dB, eB, b0)] = x1[b0];
+    }
+    wave_lds_sync();
+    FFT_STAMP(9);
+    // ---- stage B': lane (d1, beta0) gathers e1; radix-8 -> gamma0; * W_64^(gamma0 d1)
+    // (wave 0's column-0 block was written by both tasks: both writes precede
+    // these reads).  B' and C' are software-pipelined like A and B.
+    {
+        const int d1 = lane & 7, b0 = lane >> 3;  // stage-B' lane
+        const int rb0 = lane & 7, rg0 = lane >> 3; // stage-C' lane rho = beta0 + 8 gamma0
+#pragma unroll
+        for (int e1 = 0; e1 < 8; ++e1) x0[e1] = blk0[fx3(d1, e1, b0)];
+#pragma unroll
+        for (int e1 = 0; e1 < 8; ++e1) x1[e1] = blk1[fx3(d1, e1, b0)];
+        if constexpr (kOut == kFftOutSym && kReuseTw) {
+#pragma unroll
+            for (int r = 1; r < 8; ++r) tws[r] = tws_b[r]; // registers to spare in this form
+        } else {
+            powers8(twl[512 + 8 * d1], tws);
+        }
+        dft8(x0);
+        twiddle8(x0, tws);
+#pragma unroll
+        for (int g0 = 0; g0 < 8; ++g0) blk0[fx4(d1, b0, g0)] = x0[g0];
+        wave_lds_sync();
+#pragma unroll
+        for (int dd = 0; dd < 8; ++dd) x0[dd] = blk0[fx4(dd, rb0, rg0)];
+        __builtin_amdgcn_sched_barrier(0);
+        dft8(x1);
+        twiddle8(x1, tws);
+#pragma unroll
+        for (int g0 = 0; g0 < 8; ++g0) blk1[fx4(d1, b0, g0)] = x1[g0];
+        wave_lds_sync();
+#pragma unroll
+        for (int dd = 0; dd < 8; ++dd) x1[dd] = blk1[fx4(dd, rb0, rg0)];
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    FFT_STAMP(10);
+    // ---- stage C': lane rho = beta0 + 8 gamma0 has gathered d1; radix-8 -> gamma1
+    dft8(x0);
+#pragma unroll
+    for (int g1 = 0; g1 < 8; ++g1) blk0[lane + 64 * g1] = x0[g1]; // b = lane + 64 gamma1
+    __builtin_amdgcn_sched_barrier(0);
+    dft8(x1);
+#pragma unroll
+    for (int g1 = 0; g1 < 8; ++g1) blk1[lane + 64 * g1] = x1[g1];
+    FFT_STAMP(11);
+}
+
 // Persistent: one workgroup per CU walks the units u = blockIdx.x + i * gridDim.x
 // of the nch x nseg (channel, segment) grid.  The next unit's samples are
 // loaded during the current unit's final phase, so HBM latency is off the path.
@@ -737,11 +975,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     // unit instead of being hoisted out of the loop (keeps pressure down).
     int j = threadIdx.x;
     asm volatile("" : "+v"(j));
-    const int lane = j & 63;
-    const int w = j >> 6;
-    // the wave's two columns {w, 16 - w} (wave 0: {0, 8}) in adjacent slots
-    double2 *blk0 = flds + 512 * (2 * w);
-    double2 *blk1 = blk0 + 512;
+    const int w = j >> 6; // the wave: its columns {w, 16 - w} (wave 0: {0, 8}), fft_columns
     const int ch = fft_div(u, gd);
     const int64_t n0 = p.seg0 + (int64_t)(u - ch * gd.nseg) * B;
     FFT_STAMP(0);
@@ -772,208 +1006,15 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
         FFT_STAMP(4);
     }
 
-    double2 x0[8], x1[8]; // the wave's two columns (later: tasks A and B)
-    double2 tws[8];
-    // Stages A and B run as a two-column software pipeline: a column's
-    // exchange reads are issued right behind its writes, and the other
-    // column's arithmetic covers their latency (counted lgkmcnt waits).
-    // ---- stage A: lane l holds b = l + 64 t; radix-8 over t -> d1; * W_512^(l d1)
-    const int l1 = lane & 7, d1s = lane >> 3; // the stage-B lane (l1, d1)
-#pragma unroll
-    for (int t = 0; t < 8; ++t) x0[t] = blk0[lane + 64 * t];
-#pragma unroll
-    for (int t = 0; t < 8; ++t) x1[t] = blk1[lane + 64 * t];
-    powers8(twl[512 + lane], tws);
-    double2 tws_a[8]; // W_512^(lane r): stage A' of task A needs the same powers (waves 1..7, wave 0 lanes < 32)
-    if constexpr (kOut == kFftOutSym) {
-#pragma unroll
-        for (int r = 1; r < 8; ++r) tws_a[r] = tws[r];
-    }
-    dft8(x0);
-    twiddle8(x0, tws);
-#pragma unroll
-    for (int d1 = 0; d1 < 8; ++d1) blk0[fx1(lane, d1)] = x0[d1];
-    wave_lds_sync();
-#pragma unroll
-    for (int l2 = 0; l2 < 8; ++l2) x0[l2] = blk0[fx1(l1 + 8 * l2, d1s)];
-    __builtin_amdgcn_sched_barrier(0);
-    dft8(x1);
-    twiddle8(x1, tws);
-#pragma unroll
-    for (int d1 = 0; d1 < 8; ++d1) blk1[fx1(lane, d1)] = x1[d1];
-    wave_lds_sync();
-#pragma unroll
-    for (int l2 = 0; l2 < 8; ++l2) x1[l2] = blk1[fx1(l1 + 8 * l2, d1s)];
-    __builtin_amdgcn_sched_barrier(0);
-    FFT_STAMP(5);
-    // ---- stage B: lane (l1, d1) has gathered l2; radix-8 -> e1; * W_64^(l1 e1)
-    powers8(twl[512 + 8 * l1], tws);
-    double2 tws_b[8]; // W_64^(l1 r): stage B' (d1 = lane & 7 = l1) needs the same powers
-    if constexpr (kOut == kFftOutSym) {
-#pragma unroll
-        for (int r = 1; r < 8; ++r) tws_b[r] = tws[r];
-    }
-    dft8(x0);
-    twiddle8(x0, tws);
-#pragma unroll
-    for (int e1 = 0; e1 < 8; ++e1) blk0[fx2(l1, d1s, e1)] = x0[e1];
-    __builtin_amdgcn_sched_barrier(0);
-    dft8(x1);
-    twiddle8(x1, tws);
-#pragma unroll
-    for (int e1 = 0; e1 < 8; ++e1) blk1[fx2(l1, d1s, e1)] = x1[e1];
-    wave_lds_sync();
-    FFT_STAMP(6);
-    // ---- pair-table loads, issued ahead of stage C (L2 latency off the path)
-    constexpr bool kSym = kOut == kFftOutSym;
-    double2 qs[kSym ? 1 : 8], qd[kSym ? 1 : 8]; // 2 S and 2 D of the pair in slot i
-    double2 qpq[kSym ? 8 : 1], qp2[kSym ? 4 : 1]; // kSym: (p1, q2) of slot i, p2 of slots 2m, 2m+1
-    double2 wbase;                                // W_L^k of slot 0 (general form)
-    if constexpr (kSym) {
-        const double2 *t = pair + j;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) qpq[i] = t[kFftSymPQ + 512 * i]; // one 16-byte load per slot
-#pragma unroll
-        for (int m = 0; m < 4; ++m) qp2[m] = t[kFftSymP2 + 512 * m];
-    } else {
-        const double2 *t = pair + j;
-        wbase = pair[2 * kFftPairSlots * 512 + j];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            qs[i] = t[512 * i];
-            qd[i] = t[kFftPairSlots * 512 + 512 * i];
-        }
-    }
-    __builtin_amdgcn_sched_barrier(0); // keep the loads ahead of stage C
-    // ---- stage C: per task, radix-8 over l1 -> e2: x0[e2] = X[kA], x1[e2] = X[kB]
-    const uint32_t tk = tk_all;
-    const int cA = tk & 15, dA = (tk >> 4) & 7, eA = (tk >> 7) & 7; // cA, cB: LDS slots
-    const int cB = (tk >> 10) & 15, dB = (tk >> 14) & 7, eB = (tk >> 17) & 7;
-    {
-        const double2 *ba = flds + 512 * cA, *bb = flds + 512 * cB;
-#pragma unroll
-        for (int l1 = 0; l1 < 8; ++l1) x0[l1] = ba[fx2(l1, dA, eA)];
-#pragma unroll
-        for (int l1 = 0; l1 < 8; ++l1) x1[l1] = bb[fx2(l1, dB, eB)];
-    }
-    dft8(x0);
-    dft8(x1);
-    FFT_STAMP(7);
-    // ---- pair step in registers: pairs (x0[i], x1[7-i]); outputs conj(V).
-    // The real split, the multiply by G and the merge collapse to
-    //   conj(V_k) = conj(Z_k P1 + conj(Z_{M-k}) P2),  conj(V_{M-k}) = conj(Z_{M-k}) Q2 - Z_k P2
-    // with S = G_k + conj(G_{M-k}), D = G_k - conj(G_{M-k}), W = W_L^k:
-    //   P1 = 2 (S + D Im W),  P2 = 2i D Re W,  Q2 = 2 (S - D Im W)
-    // General form: the table holds 2S and 2D per (slot, thread) (host, long
-    // double) and W comes from one per-thread base times W_16^i.  Zero-phase
-    // form: the table holds P1 = p1, Q2 = q2 and P2 / i = p2 per bin.
-    {
-        // Wave 0 (a scalar, wave-uniform branch) permutes its special lane
-        // into the generic layout first (fft_w0_permute_in).
-        const bool w0 = __builtin_amdgcn_readfirstlane(w) == 0;
-        const bool sp = w0 && lane == kFftSpecialLane;
-        double2 wb_hi = wbase; // W base of slots 4..7 (general form; the zero-phase table has per-bin p1, q2, p2)
-        double2 v4 = x1[4];    // special lane: B_4, bin M/2 (slot 8, W = -i): P1 = 2S - 2D, P2 = 0
-        if (w0) {
-            v4 = cconj(cmul(v4, c8)); // a kernel argument (SGPRs: no L2 wait here)
-            if constexpr (!kSym) wb_hi = csel(sp, make_double2(0.0, 1.0), wbase);
-            fft_w0_permute_in(x0, x1, sp);
-        }
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            if constexpr (kSym)
-                fft_pair_sym(x0[i], x1[7 - i], qpq[i].x, qpq[i].y, (i & 1) ? qp2[i >> 1].y : qp2[i >> 1].x, x0[i],
-                             x1[7 - i]);
-            else
-                fft_pair(x0[i], x1[7 - i], fft_pair_w(i < 4 ? wbase : wb_hi, i), qs[i], qd[i], x0[i],
-                         x1[7 - i]);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        if (w0) fft_w0_permute_out(x0, x1, sp, v4);
-    }
-
-    FFT_STAMP(8);
-    // ---- prefetch the next unit's samples (consumed by its stage 1).
-    // Unconditional (the last unit reloads itself): a conditional load would
-    // keep the old v live across the whole loop body.
-    {
+    fft_columns<kOut>(flds, twl, pair, tk_all, c8, false, j, rnd, [&] {
+        // ---- prefetch the next unit's samples (consumed by its stage 1).
+        // Unconditional (the last unit reloads itself): a conditional load
+        // would keep the old v live across the whole loop body.
         const int un1 = fft_unit32(rnd + 1, blockIdx.x, gridDim.x, gd.units);
         const int un = un1 < gd.units ? un1 : u;
         const int cn = fft_div(un, gd);
         fft_load_unit(p, cn, p.seg0 + (int64_t)(un - cn * gd.nseg) * B, j, v);
-    }
-
-    // ---- inverse stage A': per task radix-8 over e2 -> beta0; * W_512^(beta0 d')
-    {
-        double2 *ba = flds + 512 * cA, *bb = flds + 512 * cB;
-        if constexpr (kOut == kFftOutSym) {
-            // task A's d' = dA + 8 eA is the lane except in wave 0's column-0
-            // lanes (kFftWave0C0): a wave-uniform choice
-            if (__builtin_amdgcn_readfirstlane(w) != 0) {
-#pragma unroll
-                for (int r = 1; r < 8; ++r) tws[r] = tws_a[r];
-            } else {
-                powers8(twl[512 + dA + 8 * eA], tws);
-            }
-        } else {
-            powers8(twl[512 + dA + 8 * eA], tws);
-        }
-        dft8(x0);
-        twiddle8(x0, tws);
-#pragma unroll
-        for (int b0 = 0; b0 < 8; ++b0) ba[fx3(dA, eA, b0)] = x0[b0];
-        __builtin_amdgcn_sched_barrier(0);
-        powers8(twl[512 + dB + 8 * eB], tws);
-        dft8(x1);
-        twiddle8(x1, tws);
-#pragma unroll
-        for (int b0 = 0; b0 < 8; ++b0) bb[fx3(dB, eB, b0)] = x1[b0];
-    }
-    wave_lds_sync();
-    FFT_STAMP(9);
-    // ---- stage B': lane (d1, beta0) gathers e1; radix-8 -> gamma0; * W_64^(gamma0 d1)
-    // (wave 0's column-0 block was written by both tasks: both writes precede
-    // these reads).  B' and C' are software-pipelined like A and B.
-    {
-        const int d1 = lane & 7, b0 = lane >> 3;  // stage-B' lane
-        const int rb0 = lane & 7, rg0 = lane >> 3; // stage-C' lane rho = beta0 + 8 gamma0
-#pragma unroll
-        for (int e1 = 0; e1 < 8; ++e1) x0[e1] = blk0[fx3(d1, e1, b0)];
-#pragma unroll
-        for (int e1 = 0; e1 < 8; ++e1) x1[e1] = blk1[fx3(d1, e1, b0)];
-        if constexpr (kOut == kFftOutSym) {
-#pragma unroll
-            for (int r = 1; r < 8; ++r) tws[r] = tws_b[r]; // registers to spare in this form
-        } else {
-            powers8(twl[512 + 8 * d1], tws);
-        }
-        dft8(x0);
-        twiddle8(x0, tws);
-#pragma unroll
-        for (int g0 = 0; g0 < 8; ++g0) blk0[fx4(d1, b0, g0)] = x0[g0];
-        wave_lds_sync();
-#pragma unroll
-        for (int dd = 0; dd < 8; ++dd) x0[dd] = blk0[fx4(dd, rb0, rg0)];
-        __builtin_amdgcn_sched_barrier(0);
-        dft8(x1);
-        twiddle8(x1, tws);
-#pragma unroll
-        for (int g0 = 0; g0 < 8; ++g0) blk1[fx4(d1, b0, g0)] = x1[g0];
-        wave_lds_sync();
-#pragma unroll
-        for (int dd = 0; dd < 8; ++dd) x1[dd] = blk1[fx4(dd, rb0, rg0)];
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    FFT_STAMP(10);
-    // ---- stage C': lane rho = beta0 + 8 gamma0 has gathered d1; radix-8 -> gamma1
-    dft8(x0);
-#pragma unroll
-    for (int g1 = 0; g1 < 8; ++g1) blk0[lane + 64 * g1] = x0[g1]; // b = lane + 64 gamma1
-    __builtin_amdgcn_sched_barrier(0);
-    dft8(x1);
-#pragma unroll
-    for (int g1 = 0; g1 < 8; ++g1) blk1[lane + 64 * g1] = x1[g1];
-    FFT_STAMP(11);
+    });
     if constexpr (kNrm) {
         // waves 0..3 reach this barrier well before waves 4..7: they spend
         // the wait on this unit's slice of the previous file's normalize
@@ -1021,6 +1062,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
         yb, (short)0, (int)((p.end - p.start) * 4), 0x00020000);
     // valid outputs c in [cmin, cmax): [T-1, L) for the causal table, [half,
     // L - half) for the zero-phase one (kSym: half even, fft_plan_build)
+    constexpr bool kSym = kOut == kFftOutSym;
     const int cmin = kSym ? p.half : p.ntaps - 1;
     const int cmax = kSym ? kFftL - p.half : kFftL;
     // (negative for outputs before `start`: the launch's segment grid starts
@@ -1125,6 +1167,8 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     }
 }
 
+#include "fir_fft32.hpp"
+
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
@@ -1162,34 +1206,46 @@ inline void fft_ld(std::vector<long double> &re, std::vector<long double> &im) {
 } // namespace detail
 
 
-inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, const FftTuning &tune, hipStream_t s,
-                           std::string &err) {
-    if (!fft_supported(ntaps)) {
-        err = "tap count outside the FFT method's range";
-        return false;
-    }
-    std::vector<double> taps((size_t)ntaps);
-    if (hipMemcpyAsync(taps.data(), d_taps, sizeof(double) * (size_t)ntaps, hipMemcpyDeviceToHost, s) !=
-            hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess) {
-        err = "tap download failed";
-        return false;
-    }
-    const int parts = fft_partition_count(ntaps);
+// The host-side part of an FFT plan, from the taps alone (no device): the
+// segment length, partitioning, pair tables, task words and twiddles the
+// kernels read.  tests/cpp/fft_tables_dump.cpp writes them out for the CPU
+// test that runs scripts/fft32_model.py's emulation of the kernel on them.
+struct FftTables {
+    int L = 0, halves = 1, parts = 1, tp = 0;
+    bool sym = false;
+    std::vector<double2> pair; // parts x halves x kFftPairTable
+    std::vector<uint32_t> task; // halves x 512
+    std::vector<double2> c8;   // per partition
+    std::vector<double2> tw;   // kFftTw or kFft32Tw
+};
+
+inline FftTables fft_plan_tables(const std::vector<double> &taps, const FftTuning &tune) {
+    const int ntaps = (int)taps.size();
+    // segment length: the tuning's, else by tap count; L = 32768 runs
+    // fir_fft32.hpp's two 8192-point halves (bins of each parity)
+    const int L = tune.seg_len ? tune.seg_len : fft_choose_seg_len(ntaps);
+    const int halves = L == kFft32L ? 2 : 1;
+    const int Mf = L / 2; // complex transform length
+    const int parts = fft_partition_count(ntaps, L);
     const int tp = parts == 1 ? ntaps : fft_partition_taps(ntaps, parts);
     const bool sym = fft_sym_eligible(taps, parts, tune);
-    const long double scale = 1.0L / (4.0L * (long double)kFftM);
+    const long double scale = 1.0L / (4.0L * (long double)Mf);
     const long double two_pi = 6.283185307179586476925286766559L;
     // pair tables in consumption order: slot i of thread t holds bin k_i of
     // its task A (special lane: the permuted list; slot 8: k = M/2) as the
     // collapsed split/multiply/merge coefficients 2S, 2D, plus W_L^k in the
     // third field (the kernel reads slot 0's as its W base); the zero-phase
-    // form stores fft_pair_sym's p1, q2, p2 per bin instead (kFftSymPQ, kFftSymP2)
-    std::vector<double2> pair((size_t)parts * kFftPairTable);
-    std::vector<uint32_t> task((size_t)kFftNT);
-    std::vector<double2> c8((size_t)parts);
+    // form stores fft_pair_sym's p1, q2, p2 per bin instead (kFftSymPQ, kFftSymP2).
+    // Bin kappa of an 8192-point transform is k = kappa (L = 16384) or, half h
+    // of L = 32768, k = 2 kappa + h; its partner is M - k in either case.
+    FftTables T;
+    std::vector<double2> &pair = T.pair, &c8 = T.c8;
+    std::vector<uint32_t> &task = T.task;
+    pair.resize((size_t)parts * halves * kFftPairTable);
+    task.resize((size_t)halves * kFftNT);
+    c8.resize((size_t)parts);
     auto cplx = [](long double r, long double i) { return make_double2((double)r, (double)i); };
-    std::vector<long double> re((size_t)kFftL), im((size_t)kFftL);
+    std::vector<long double> re((size_t)L), im((size_t)L);
     for (int part = 0; part < parts; ++part) {
         // G = FFT_L(g), g[j] = h_p[tp-1-j] with h_p[k] = h[part * tp + k] (0 past
         // the filter's end), zero padded; scaled by 1/(4M)
@@ -1205,44 +1261,51 @@ inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, const
             // h_sym = (h + reversed h) / 2 -- real and even, so G is real
             const int half = (ntaps - 1) / 2;
             for (int j = -half; j <= half; ++j)
-                re[(size_t)((j + kFftL) % kFftL)] =
+                re[(size_t)((j + L) % L)] =
                     ((long double)taps[(size_t)(half + j)] + (long double)taps[(size_t)(half - j)]) * 0.5L;
         }
         detail::fft_ld(re, im);
-        double2 *pt = pair.data() + (size_t)part * kFftPairTable;
-        for (int t = 0; t < kFftNT; ++t) {
-            const uint32_t tk = fft_task_word(t);
-            task[(size_t)t] = tk;
-            const int ca = fft_slot_column(tk & 15), da = (tk >> 4) & 7, ea = (tk >> 7) & 7;
-            const bool sp = t == kFftSpecialLane;
-            for (int i = 0; i < kFftPairSlots; ++i) {
-                int k;
-                if (i == 8) k = kFftM / 2;
-                else if (!sp) k = ca + 16 * (da + 8 * ea + 64 * i);
-                else k = i < 4 ? 512 + 1024 * i : 1024 * (i - 4); // fft_w0_permute_in
-                const long double gr = re[(size_t)k] * scale, gi = im[(size_t)k] * scale;
-                const long double hr = re[(size_t)(kFftM - k)] * scale, hi = -im[(size_t)(kFftM - k)] * scale;
-                const long double sr = gr + hr, si = gi + hi; // S = G_k + conj(G_{M-k})
-                const long double dr = gr - hr, di = gi - hi; // D = G_k - conj(G_{M-k})
-                const long double a = -two_pi * (long double)k / (long double)kFftL;
-                const long double c = cosl(a), sn = sinl(a); // W = c + i sn
-                const size_t o = (size_t)i * kFftNT + (size_t)t;
-                if (!sym) {
-                    pt[o] = cplx(2 * sr, 2 * si);
-                    pt[(size_t)kFftPairSlots * kFftNT + o] = cplx(2 * dr, 2 * di);
-                    pt[(size_t)2 * kFftPairSlots * kFftNT + o] = cplx(c, sn);
-                } else if (i < 8) {
-                    // zero-phase layout: p1, q2, p2 per (slot, thread) (fft_pair_sym)
-                    const long double p1 = 2 * sr + 2 * dr * sn, q2 = 2 * sr - 2 * dr * sn, p2 = 2 * dr * c;
-                    pt[(size_t)kFftSymPQ + o] = cplx(p1, q2);
-                    double *p2t = reinterpret_cast<double *>(pt + kFftSymP2 + (size_t)(i >> 1) * kFftNT + (size_t)t);
-                    p2t[i & 1] = (double)p2;
+        for (int h = 0; h < halves; ++h) {
+            double2 *pt = pair.data() + ((size_t)part * halves + (size_t)h) * kFftPairTable;
+            for (int t = 0; t < kFftNT; ++t) {
+                const uint32_t tk = h == 0 ? fft_task_word(t) : fft32_task_word_odd(t);
+                task[(size_t)h * kFftNT + (size_t)t] = tk;
+                const int ca = h == 0 ? fft_slot_column(tk & 15) : fft32_slot_odd_column(tk & 15);
+                const int da = (tk >> 4) & 7, ea = (tk >> 7) & 7;
+                const bool sp = h == 0 && t == kFftSpecialLane;
+                for (int i = 0; i < (h == 0 ? kFftPairSlots : 8); ++i) {
+                    int kap;
+                    if (i == 8) kap = kFftM / 2;
+                    else if (!sp) kap = ca + 16 * (da + 8 * ea + 64 * i);
+                    else kap = i < 4 ? 512 + 1024 * i : 1024 * (i - 4); // fft_w0_permute_in
+                    const int k = halves == 1 ? kap : 2 * kap + h;
+                    const long double gr = re[(size_t)k] * scale, gi = im[(size_t)k] * scale;
+                    const long double hr = re[(size_t)(Mf - k)] * scale, hi = -im[(size_t)(Mf - k)] * scale;
+                    const long double sr = gr + hr, si = gi + hi; // S = G_k + conj(G_{M-k})
+                    const long double dr = gr - hr, di = gi - hi; // D = G_k - conj(G_{M-k})
+                    const long double a = -two_pi * (long double)k / (long double)L;
+                    const long double c = cosl(a), sn = sinl(a); // W = c + i sn
+                    const size_t o = (size_t)i * kFftNT + (size_t)t;
+                    if (!sym) {
+                        pt[o] = cplx(2 * sr, 2 * si);
+                        pt[(size_t)kFftPairSlots * kFftNT + o] = cplx(2 * dr, 2 * di);
+                        pt[(size_t)2 * kFftPairSlots * kFftNT + o] = cplx(c, sn);
+                    } else if (i < 8) {
+                        // zero-phase layout: p1, q2, p2 per (slot, thread) (fft_pair_sym)
+                        const long double p1 = 2 * sr + 2 * dr * sn, q2 = 2 * sr - 2 * dr * sn, p2 = 2 * dr * c;
+                        pt[(size_t)kFftSymPQ + o] = cplx(p1, q2);
+                        double *p2t =
+                            reinterpret_cast<double *>(pt + kFftSymP2 + (size_t)(i >> 1) * kFftNT + (size_t)t);
+                        p2t[i & 1] = (double)p2;
+                    }
+                    if (i == 8 && sp) c8[(size_t)part] = cplx(2 * sr - 2 * dr, sym ? 0.0L : 2 * si - 2 * di);
                 }
-                if (i == 8 && sp) c8[(size_t)part] = cplx(2 * sr - 2 * dr, sym ? 0.0L : 2 * si - 2 * di);
             }
         }
     }
-    std::vector<double2> tw((size_t)kFftTw);
+    // W_8192^i (i < 512), W_512^i (i < 64); L = 32768 adds W_16384^i (i < 512)
+    std::vector<double2> &tw = T.tw;
+    tw.resize((size_t)(halves == 2 ? kFft32Tw : kFftTw));
     for (int i = 0; i < 512; ++i) {
         const long double a = -two_pi * (long double)i / 8192.0L;
         tw[(size_t)i] = make_double2((double)cosl(a), (double)sinl(a));
@@ -1251,6 +1314,35 @@ inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, const
         const long double a = -two_pi * (long double)i / 512.0L;
         tw[(size_t)(512 + i)] = make_double2((double)cosl(a), (double)sinl(a));
     }
+    if (halves == 2)
+        for (int i = 0; i < 512; ++i) {
+            const long double a = -two_pi * (long double)i / 16384.0L;
+            tw[(size_t)(kFft32TwOdd + i)] = make_double2((double)cosl(a), (double)sinl(a));
+        }
+    T.L = L;
+    T.halves = halves;
+    T.parts = parts;
+    T.tp = tp;
+    T.sym = sym;
+    return T;
+}
+
+inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, const FftTuning &tune, hipStream_t s,
+                           std::string &err) {
+    if (!fft_supported(ntaps)) {
+        err = "tap count outside the FFT method's range";
+        return false;
+    }
+    std::vector<double> taps((size_t)ntaps);
+    if (hipMemcpyAsync(taps.data(), d_taps, sizeof(double) * (size_t)ntaps, hipMemcpyDeviceToHost, s) !=
+            hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
+        err = "tap download failed";
+        return false;
+    }
+    const FftTables T = fft_plan_tables(taps, tune);
+    const std::vector<double2> &pair = T.pair, &tw = T.tw;
+    const std::vector<uint32_t> &task = T.task;
     // stream-ordered on the ctx's own stream s (freed the same way, fft_plan_free)
     if (hipMallocAsync(reinterpret_cast<void **>(&plan.d_pair), sizeof(double2) * pair.size(), s) != hipSuccess ||
         hipMallocAsync(reinterpret_cast<void **>(&plan.d_tw), sizeof(double2) * tw.size(), s) != hipSuccess ||
@@ -1273,18 +1365,21 @@ inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, const
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
         cus > 0)
         plan.cus = cus;
-    plan.ntaps = tp;
-    plan.parts = parts;
-    plan.sym = sym;
+    plan.L = T.L;
+    plan.ntaps = T.tp;
+    plan.parts = T.parts;
+    plan.sym = T.sym;
     plan.tune = tune;
-    plan.B = kFftL - tp + 1;
-    plan.c8 = std::move(c8);
+    plan.B = T.L - T.tp + 1;
+    plan.c8 = T.c8;
     plan.ready = true;
     return true;
 }
 
-// work array + twiddles + one f32 peak slot per wave
-constexpr size_t fft_lds_bytes() { return sizeof(double2) * (size_t)(kFftM + kFftTw) + 4 * (kFftNT / 64); }
+// work array + twiddles + one f32 peak slot per wave (L = 32768: 145 KiB)
+constexpr size_t fft_lds_bytes(int L = 16384) {
+    return sizeof(double2) * (size_t)(kFftM + (L == kFft32L ? kFft32Tw : kFftTw)) + 4 * (kFftNT / 64);
+}
 
 // Outputs per launch.  The kernel addresses samples and outputs through raw
 // buffer resources with 32-bit byte offsets (and 0x80000000 as its "drop this
@@ -1297,9 +1392,38 @@ inline int64_t fft_chunk(const FftPlan &plan) {
     return plan.tune.chunk >= 4096 ? plan.tune.chunk : ((int64_t)1 << 28);
 }
 
+template <int kOut>
+inline bool fft32_launch_one(const FftPlan &plan, const DirectParams &q, int part, int nch, hipStream_t s,
+                             std::string &err) {
+    static const bool attr = [] {
+        return hipFuncSetAttribute(reinterpret_cast<const void *>(&fir_fft32_f64_kernel<kOut>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)fft_lds_bytes(kFft32L)) == hipSuccess;
+    }();
+    (void)attr;
+    const int64_t nseg = (q.end - q.seg0 + plan.B - 1) / plan.B;
+    const int64_t units = nseg * nch; // < 2^31 (fft_launch)
+    const int64_t grid = std::min<int64_t>(units, (int64_t)plan.cus); // one 145 KiB workgroup per CU
+    if (!q.park && kParkSlab > 0) {
+        err = "L = 32768 launch without its park slab";
+        return false;
+    }
+    hipLaunchKernelGGL((fir_fft32_f64_kernel<kOut>), dim3((unsigned)grid), dim3(kFftNT), fft_lds_bytes(kFft32L), s,
+                       q, plan.d_pair + (size_t)part * 2 * kFftPairTable, plan.d_tw, plan.d_task, plan.B,
+                       fft_grid(nseg, units), plan.c8[(size_t)part]);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        err = hipGetErrorString(e);
+        return false;
+    }
+    return true;
+}
+
 template <int kOut, bool kNrm = false>
 inline bool fft_launch_one(const FftPlan &plan, const DirectParams &q, int part, int nch, hipStream_t s,
                            std::string &err, FftNrm nrm = FftNrm{}) {
+    if constexpr (!kNrm)
+        if (plan.L == kFft32L) return fft32_launch_one<kOut>(plan, q, part, nch, s, err);
     static const bool attr = [] {
         return hipFuncSetAttribute(reinterpret_cast<const void *>(&fir_fft_f64_kernel<kOut, kNrm>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1360,7 +1484,7 @@ inline void fft_window(const FftPlan &plan, int64_t half, int64_t start, int64_t
     const int64_t g0 = fft_grid_start(plan, start);
     const int64_t last = g0 + std::max<int64_t>(0, (end - g0 + plan.B - 1) / plan.B - 1) * plan.B;
     lo = g0 - half;
-    hi = last - half + (int64_t)(plan.parts - 1) * plan.ntaps + kFftL;
+    hi = last - half + (int64_t)(plan.parts - 1) * plan.ntaps + plan.L;
 }
 // Segments of the first launch chunk of [p.start, p.end)
 inline int64_t fft_first_nseg(const FftPlan &plan, const DirectParams &p) {
@@ -1372,6 +1496,11 @@ inline int64_t fft_first_nseg(const FftPlan &plan, const DirectParams &p) {
 inline size_t fft_scratch_doubles(const FftPlan &plan, const DirectParams &p, int nch) {
     if (plan.parts == 1 || p.end <= p.start) return 0;
     return (size_t)std::min<int64_t>(p.end - p.start, fft_chunk_span(plan)) * (size_t)std::max(nch, 1);
+}
+// Doubles of park slab an L = 32768 launch needs (one slab per workgroup of
+// the persistent grid, fir_fft32.hpp); launches on one stream reuse it.
+inline size_t fft32_park_doubles(const FftPlan &plan) {
+    return plan.L == kFft32L ? (size_t)plan.cus * kParkSlab * kFftNT * 2 : 0;
 }
 
 // Filter outputs [p.start, p.end) of nch channels.  p.half / p.ntaps are the
@@ -1392,7 +1521,7 @@ inline bool fft_launch_group(const FftPlan &plan, const DirectParams &p, int nch
 // The first launch (the one that carries it) must spread the previous
 // file's floats at <= kNrmK x 1 024 per unit.
 inline bool fft_nrm_fusable(const FftPlan &plan, const FftNrm &nrm, const DirectParams &p, int nch) {
-    if (plan.parts != 1 || !nrm.y || !nrm.peak || nrm.npeak < 1 ||
+    if (plan.parts != 1 || plan.L != kFftL || !nrm.y || !nrm.peak || nrm.npeak < 1 ||
         (reinterpret_cast<uintptr_t>(nrm.y) & 15) != 0 || p.end <= p.start || nch <= 0)
         return false;
     const int64_t nseg = fft_first_nseg(plan, p);

@@ -199,14 +199,19 @@ int run_filter(lcfir_ctx *ctx, lcfir::DirectParams p, int nch, hipStream_t s,
         int rc = ensure_fft(ctx);
         if (rc) return rc;
         std::string err;
-        if (ctx->fft.parts > 1) {
-            const size_t need = lcfir::fft_scratch_doubles(ctx->fft, p, nch);
+        // per-stream scratch: the L = 32768 kernel's park slabs, then the
+        // partitioned filters' f64 partial sums
+        const size_t npark = lcfir::fft32_park_doubles(ctx->fft);
+        const size_t need = npark + lcfir::fft_scratch_doubles(ctx->fft, p, nch);
+        if (need > 0) {
             bool capture_error = false;
-            p.y64 = stream_scratch(ctx, s, need, capture_error);
+            double *base = stream_scratch(ctx, s, need, capture_error);
             if (capture_error)
-                return fail(LCFIR_EINVAL, "partial-sum scratch of %zu doubles is not allocated on this stream: run "
+                return fail(LCFIR_EINVAL, "FFT scratch of %zu doubles is not allocated on this stream: run "
                             "an eager call of this shape on it before HIP graph capture", need);
-            if (!p.y64) return fail(LCFIR_ENOMEM, "partial-sum scratch of %zu doubles", need);
+            if (!base) return fail(LCFIR_ENOMEM, "FFT scratch of %zu doubles", need);
+            p.park = npark ? reinterpret_cast<double2 *>(base) : nullptr;
+            p.y64 = ctx->fft.parts > 1 ? base + npark : nullptr;
         }
         const bool fuse = nrm && lcfir::fft_nrm_fusable(ctx->fft, *nrm, p, nch);
         if (!lcfir::fft_launch(ctx->fft, p, nch, s, err, fuse ? nrm : nullptr))
@@ -431,7 +436,7 @@ int lcfir_ctx_fft_info(lcfir_ctx *ctx, int32_t *seg_len, int32_t *parts, int32_t
     if (!g.ok) return fail(LCFIR_EDEVICE, "hipSetDevice(%d) failed", ctx->device);
     const int rc = ensure_fft(ctx);
     if (rc != LCFIR_OK) return rc;
-    *seg_len = lcfir::kFftL;
+    *seg_len = ctx->fft.L;
     *parts = ctx->fft.parts;
     *zero_phase = ctx->fft.sym ? 1 : 0;
     return LCFIR_OK;
@@ -440,8 +445,9 @@ int lcfir_ctx_fft_info(lcfir_ctx *ctx, int32_t *seg_len, int32_t *parts, int32_t
 int lcfir_ctx_set_fft_tuning(lcfir_ctx *ctx, int32_t seg_len, int32_t zero_phase, int64_t chunk,
                              int64_t max_units) {
     if (!ctx) return fail(LCFIR_EINVAL, "ctx is null");
-    if (seg_len != 0 && seg_len != lcfir::kFftL)
-        return fail(LCFIR_EINVAL, "segment length %d not supported (0 or %d)", seg_len, lcfir::kFftL);
+    if (seg_len != 0 && seg_len != lcfir::kFftL && seg_len != lcfir::kFft32L)
+        return fail(LCFIR_EINVAL, "segment length %d not supported (0, %d or %d)", seg_len, lcfir::kFftL,
+                    lcfir::kFft32L);
     if (zero_phase != 0 && zero_phase != 1) return fail(LCFIR_EINVAL, "zero_phase must be 0 or 1");
     if (chunk != 0 && chunk < 4096) return fail(LCFIR_EINVAL, "chunk must be 0 or >= 4096 outputs");
     if (max_units < 0 || max_units >= ((int64_t)1 << 31)) return fail(LCFIR_EINVAL, "max_units out of range");
@@ -456,6 +462,7 @@ int lcfir_ctx_set_fft_tuning(lcfir_ctx *ctx, int32_t seg_len, int32_t zero_phase
     }
     lcfir::fft_plan_free(ctx->fft, ctx->own);
     LCFIR_HIP(hipStreamSynchronize(ctx->own));
+    ctx->tune.seg_len = seg_len;
     ctx->tune.zero_phase = zero_phase;
     ctx->tune.chunk = chunk;
     ctx->tune.max_units = max_units;

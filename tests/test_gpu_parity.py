@@ -534,3 +534,68 @@ def test_staging_pool_cap_release_and_ctx_destroy(lc, oracle_mod):
     flt.close()
     ref = oracle_mod.filter_channel(x, taps, oracle_mod.MODE_LD)
     assert rms(whole, ref) <= RMS_TOL and max_ulps(whole, ref) <= 1
+
+
+# ---- the L = 32 768 segment (fir_fft32.hpp): both halves, every output form
+@pytest.mark.parametrize("ntaps,perturb", [(4001, 0.0), (4003, 0.0), (8001, 0.0), (8001, 1e-9), (19201, 0.0),
+                                           (38401, 0.0), (100001, 0.0)])
+def test_fft_seg32_forms(lc, oracle_mod, ntaps, perturb):
+    """The 32 768-sample segment (two 8192-point halves split by bin parity,
+    park slab, radix-2 merge) forced by lcfir_ctx_set_fft_tuning, for the
+    zero-phase (4001, 8001, 19201 taps: one partition), general (4003: odd
+    half; 8001 with a visible antisymmetric part) and partitioned (38401,
+    100001) forms: against the long-double oracle at every edge sample and
+    random positions, within 1 ulp of the 16 384-sample segment, windowed calls
+    bit-identical to the whole channel, the reference's thread hand-off
+    bit-identical, peaks fused."""
+    import synth
+    fs, n = 48000.0, 300_001
+    taps = oracle_mod.design_lowcut(20.0, fs, ntaps)
+    if perturb:
+        taps = taps + perturb * np.linspace(-1.0, 1.0, ntaps)
+    x = synth.file_buffer(2, n, fs, file=11, bits=24)
+    flt = lc.Filter(taps, method="fft")
+    flt.set_fft_tuning(seg_len=32768)
+    info = flt.fft_info
+    assert info["seg_len"] == 32768
+    assert info["zero_phase"] == (perturb == 0.0 and ntaps in (4001, 8001, 19201))
+    y, pk = gpu_filter_channels(lc, flt, x)
+    half = (ntaps - 1) // 2
+    for c in range(2):
+        idx = _sample_positions(n, half, 2048, 900 + c)
+        ref_ld, _ = oracle_mod.filter_points(x[c], taps, idx, oracle_mod.MODE_LD)
+        assert rms(y[c][idx], ref_ld) <= RMS_TOL, c
+        assert max_ulps(y[c][idx], ref_ld) <= 1, c
+        assert pk[c] == np.abs(y[c]).max()
+    f16 = lc.Filter(taps, method="fft")
+    f16.set_fft_tuning(seg_len=16384)
+    y16, _ = gpu_filter_channels(lc, f16, x)
+    assert max_ulps(y, y16) <= 1 and rms(y, y16) <= RMS_TOL
+    for start, end in [(1, n - 1), (half + 3, half + 40_000), (123_457, 123_458), (n - 33_000, n)]:
+        check_window(lc, flt, x, y, start, end)
+    for threads in (3, 7):
+        assert np.array_equal(lc.filter_channel(x[0], flt, threads), y[0]), threads
+
+
+def test_fft_seg32_chunks_and_groups(lc, oracle_mod):
+    """The 32 768-sample segment under launch chunks of whole segments and
+    channel groups (lcfir_ctx_set_fft_tuning chunk / max_units): bytes and
+    peaks identical to one launch; a channel shorter than one segment and a
+    one-sample channel."""
+    import synth
+    taps = oracle_mod.design_lowcut(20.0, 96000.0, 8001)
+    x = synth.file_buffer(5, 200_003, 96000.0, file=12, bits=None)
+    one = lc.Filter(taps, method="fft")
+    one.set_fft_tuning(seg_len=32768)
+    y0, pk0 = gpu_filter_channels(lc, one, x)
+    for chunk, mu in [(70_000, 0), (0, 9), (50_000, 4)]:
+        f = lc.Filter(taps, method="fft")
+        f.set_fft_tuning(seg_len=32768, chunk=chunk, max_units=mu)
+        y1, pk1 = gpu_filter_channels(lc, f, x)
+        assert np.array_equal(y0, y1) and np.array_equal(pk0, pk1), (chunk, mu)
+    for n in (20_000, 1):
+        xs = np.ascontiguousarray(x[:2, :n])
+        ys, _ = gpu_filter_channels(lc, one, xs)
+        for c in range(2):
+            ref = oracle_mod.filter_channel(xs[c], taps, oracle_mod.MODE_LD)
+            assert max_ulps(ys[c], ref) <= 1 and rms(ys[c], ref) <= RMS_TOL, (n, c)
