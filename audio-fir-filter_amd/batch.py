@@ -343,9 +343,21 @@ class DeviceBackend(Backend):
         self.streams += [torch.cuda.Stream(device) for _ in range(lanes - 1)]
         self.stream = self.streams[0]
         self.sp = self.stream.cuda_stream
+        # one-graph replays (GraphedSteps.replay) run every lane's steps on
+        # lane 0's stream: `dirty` = lanes given eager work since the last
+        # replay (the replay waits for them), `graph_waiters` = lanes whose
+        # next eager work must wait for the last replay.  Both waits are taken
+        # lazily, only for lanes that actually mix eager and replayed steps
+        # (each wait costs host time a launch-bound replay cannot spare).
+        self.dirty = set()
+        self.graph_waiters = set()
 
     def set_lane(self, lane):
         s = self.streams[lane]
+        if lane in self.graph_waiters:
+            self.graph_waiters.discard(lane)
+            s.wait_stream(self.streams[0])
+        self.dirty.add(lane)
         self.stream, self.sp = s, s.cuda_stream
         # torch-side work of the step (the RCCL peak exchange) follows the lane
         self.torch.cuda.set_stream(s)
@@ -471,21 +483,25 @@ class GraphedSteps:
     def replay(self):
         """Run per_replay steps, each graph on its lane's stream (the caller
         syncs).  One-graph mode: the graph is launched on lane 0's stream but
-        runs every lane's steps, so lane 0 first waits for work already queued
-        on the other lanes, and the other lanes then wait for the graph, so
-        eager steps before and after a replay stay in order on every lane."""
+        runs every lane's steps, so lane 0 first waits for eager work queued
+        on the other lanes since the last replay (DeviceBackend.dirty), and
+        each other lane's next eager step waits for the graph
+        (DeviceBackend.graph_waiters, taken in set_lane): eager steps before
+        and after a replay stay in order on every lane, and back-to-back
+        replays pay no waits."""
         torch = self.backend.torch
-        one = len(self.graphs) == 1 and len(self.backend.streams) > 1
-        s0 = self.backend.streams[0]
+        b = self.backend
+        one = len(self.graphs) == 1 and len(b.streams) > 1
+        s0 = b.streams[0]
         if one:
-            for s in self.backend.streams[1:]:
-                s0.wait_stream(s)
+            for lane in sorted(b.dirty - {0}):
+                s0.wait_stream(b.streams[lane])
+            b.dirty.clear()
         for s, g in self.graphs:
             with torch.cuda.stream(s):
                 g.replay()
         if one:
-            for s in self.backend.streams[1:]:
-                s.wait_stream(s0)
+            b.graph_waiters = set(range(1, len(b.streams)))
 
 
 def torch_allreduce_max(group=None):

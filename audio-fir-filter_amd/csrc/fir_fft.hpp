@@ -194,18 +194,50 @@ inline int fft_partition_count(int ntaps, int L = 16384) {
     }
     return best;
 }
-// Relative cost of one L = 32 768 segment (fir_fft32.hpp: two 8192-point
-// halves plus the radix-2 split and merge) against one L = 16 384 segment:
-// f64 instructions per thread, 3 348 against 1 470.
-constexpr double kFft32SegCost = 2.28;
-// Segment length for a filter: the one with the lower estimated work per
-// output, cost(L) x parts / (L - taps + 1); the longer segment only when it
-// saves at least 5 % (the L = 16 384 kernel also carries a fused normalize).
-inline int fft_choose_seg_len(int ntaps) {
-    const int p16 = fft_partition_count(ntaps, 16384), p32 = fft_partition_count(ntaps, 32768);
-    const double c16 = (double)p16 / (double)(16384 - fft_partition_taps(ntaps, p16) + 1);
-    const double c32 = kFft32SegCost * p32 / (double)(32768 - fft_partition_taps(ntaps, p32) + 1);
+// The launch a plan is chosen for (fft_choose_seg_len): outputs per channel
+// and channels of the first call that builds it, and the device's CUs.
+// outputs = 0: no call known (the per-output cost decides).
+struct FftShape {
+    int64_t outputs = 0;
+    int nch = 1;
+    int cus = 256;
+};
+// Time of one unit relative to a single-partition L = 16 384 unit, measured
+// on MI355X with tools/fft32_trace.hip (config-3 shape, 6 001 .. 30 001 taps,
+// DESIGN.md s4.2): a partitioned L = 16 384 pass also reads and writes its f64
+// partial sums; an L = 32 768 unit is two 8192-point halves plus the split,
+// the merge and the park slab, the general pair table and partitions cost
+// more there (register pressure).
+inline double fft_unit_cost(int L, int parts, bool sym) {
+    if (L == 16384) return parts == 1 ? 1.0 : 1.25;
+    return parts == 1 ? (sym ? 2.9 : 3.1) : 4.0;
+}
+// Estimated time of a launch of `shape` with segment length L: partitions x
+// rounds of the persistent grid x unit cost (or, without a shape, the cost per
+// output).  Infinity when L cannot hold the filter.
+inline double fft_seg_estimate(const std::vector<double> &h, int L, const FftShape &shape, const FftTuning &tune);
+// Segment length for a filter (FftTuning::seg_len = 0): the lower estimate
+// for the first call's shape, the longer segment only when it saves at least
+// 5 %.  Per filter, not per call: the segment grid must not change under a
+// ctx (partition invariance, fft_grid_start).  Long launches of long filters
+// take L = 32 768 (one partition up to 30 721 taps instead of two from
+// 10 900, 2x faster at 12 001 .. 19 201 taps); short ones, where a 2.9x longer
+// unit is the whole launch, keep L = 16 384 (config 1: 48 000 samples).
+inline int fft_choose_seg_len(const std::vector<double> &h, const FftShape &shape, const FftTuning &tune) {
+    const double c16 = fft_seg_estimate(h, 16384, shape, tune), c32 = fft_seg_estimate(h, 32768, shape, tune);
     return c32 < 0.95 * c16 ? 32768 : 16384;
+}
+
+inline double fft_seg_estimate(const std::vector<double> &h, int L, const FftShape &shape, const FftTuning &tune) {
+    const int ntaps = (int)h.size();
+    const int parts = fft_partition_count(ntaps, L);
+    if (parts == 0) return 1e300;
+    const int B = L - (parts == 1 ? ntaps : fft_partition_taps(ntaps, parts)) + 1;
+    const double unit = fft_unit_cost(L, parts, fft_sym_eligible(h, parts, tune));
+    if (shape.outputs <= 0) return unit * parts / (double)B;
+    const int64_t units = (int64_t)std::max(shape.nch, 1) * ((shape.outputs + B - 1) / B);
+    const int cus = std::max(shape.cus, 1);
+    return unit * parts * (double)((units + cus - 1) / cus);
 }
 
 // LDS slot of column c: a wave's two columns sit in adjacent 8 KiB blocks
@@ -1219,11 +1251,12 @@ struct FftTables {
     std::vector<double2> tw;   // kFftTw or kFft32Tw
 };
 
-inline FftTables fft_plan_tables(const std::vector<double> &taps, const FftTuning &tune) {
+inline FftTables fft_plan_tables(const std::vector<double> &taps, const FftTuning &tune,
+                                 const FftShape &shape = FftShape{}) {
     const int ntaps = (int)taps.size();
-    // segment length: the tuning's, else by tap count; L = 32768 runs
-    // fir_fft32.hpp's two 8192-point halves (bins of each parity)
-    const int L = tune.seg_len ? tune.seg_len : fft_choose_seg_len(ntaps);
+    // segment length: the tuning's, else the estimate's for the first call's
+    // shape; L = 32768 runs fir_fft32.hpp's two 8192-point halves (bins of each parity)
+    const int L = tune.seg_len ? tune.seg_len : fft_choose_seg_len(taps, shape, tune);
     const int halves = L == kFft32L ? 2 : 1;
     const int Mf = L / 2; // complex transform length
     const int parts = fft_partition_count(ntaps, L);
@@ -1328,7 +1361,7 @@ inline FftTables fft_plan_tables(const std::vector<double> &taps, const FftTunin
 }
 
 inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, const FftTuning &tune, hipStream_t s,
-                           std::string &err) {
+                           std::string &err, FftShape shape = FftShape{}) {
     if (!fft_supported(ntaps)) {
         err = "tap count outside the FFT method's range";
         return false;
@@ -1340,7 +1373,13 @@ inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, const
         err = "tap download failed";
         return false;
     }
-    const FftTables T = fft_plan_tables(taps, tune);
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        cus > 0)
+        plan.cus = cus;
+    shape.cus = plan.cus;
+    const FftTables T = fft_plan_tables(taps, tune, shape);
     const std::vector<double2> &pair = T.pair, &tw = T.tw;
     const std::vector<uint32_t> &task = T.task;
     // stream-ordered on the ctx's own stream s (freed the same way, fft_plan_free)
@@ -1360,11 +1399,6 @@ inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, const
         err = "FFT plan upload failed";
         return false;
     }
-    int dev = 0, cus = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-        cus > 0)
-        plan.cus = cus;
     plan.L = T.L;
     plan.ntaps = T.tp;
     plan.parts = T.parts;

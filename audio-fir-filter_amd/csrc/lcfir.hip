@@ -122,11 +122,17 @@ int resolve_method(lcfir_ctx *ctx) {
     return lcfir::fft_preferred(ctx->ntaps) ? LCFIR_METHOD_FFT : LCFIR_METHOD_DIRECT;
 }
 
-int ensure_fft(lcfir_ctx *ctx) {
+// The FFT plan, built at the first use: its segment length (unless tuned) is
+// chosen for that call's shape, outputs per channel x nch (0: unknown),
+// lcfir::fft_choose_seg_len
+int ensure_fft(lcfir_ctx *ctx, int64_t outputs = 0, int nch = 1) {
     std::lock_guard<std::mutex> lk(ctx->fft_mu);
     if (ctx->fft.ready) return LCFIR_OK;
     std::string err;
-    if (!lcfir::fft_plan_build(ctx->fft, ctx->d_taps, ctx->ntaps, ctx->tune, ctx->own, err))
+    lcfir::FftShape shape;
+    shape.outputs = outputs;
+    shape.nch = nch;
+    if (!lcfir::fft_plan_build(ctx->fft, ctx->d_taps, ctx->ntaps, ctx->tune, ctx->own, err, shape))
         return fail(LCFIR_EDEVICE, "fft plan: %s", err.c_str());
     return LCFIR_OK;
 }
@@ -196,7 +202,7 @@ int run_filter(lcfir_ctx *ctx, lcfir::DirectParams p, int nch, hipStream_t s,
     if (track_stream) note_stream(ctx, s);
     const int m = resolve_method(ctx);
     if (m == LCFIR_METHOD_FFT) {
-        int rc = ensure_fft(ctx);
+        int rc = ensure_fft(ctx, p.end - p.start, nch);
         if (rc) return rc;
         std::string err;
         // per-stream scratch: the L = 32768 kernel's park slabs, then the
@@ -474,7 +480,7 @@ static int range_window(lcfir_ctx *ctx, int64_t n, int64_t start, int64_t end, i
     lo = start - ctx->half;
     hi = end + ctx->half;
     if (resolve_method(ctx) == LCFIR_METHOD_FFT) {
-        const int rc = ensure_fft(ctx);
+        const int rc = ensure_fft(ctx, end - start, 1);
         if (rc) return rc;
         lcfir::fft_window(ctx->fft, ctx->half, start, end, lo, hi);
     }

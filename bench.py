@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--channels", type=int, default=2)
     ap.add_argument("--fs", type=float, default=48000.0)
     ap.add_argument("--ntaps", type=int, default=4001)
+    ap.add_argument("--seg-len", type=int, default=0, choices=[0, 16384, 32768],
+                    help="FFT segment length (0 = the library's choice by tap count)")
     ap.add_argument("--bits", type=int, default=24, help="0 = float32 source")
     ap.add_argument("--normalize", action="store_true")
     ap.add_argument("--peak-scope", default="file", choices=["file", "global"])
@@ -77,6 +79,9 @@ def parse():
     ap.add_argument("--kernel-launches", type=int, default=20,
                     help="launches of the filter alone, one stream, right after the pre-roll: "
                          "the exclusive kernel time roofline.kernel_ms is measured on")
+    ap.add_argument("--force-exchange", action="store_true",
+                    help="run the peak all-reduce every step even where the plan needs none (at --gpus 1: "
+                         "a world-1 RCCL group; config 5 --files 1 is then the N = 8 per-rank step)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
@@ -320,6 +325,13 @@ def main():
             dist.init_process_group("gloo", rank=rank, world_size=world)
         else:
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    elif args.force_exchange:
+        import socket
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                device_id=dev)
 
     import lcfir   # after torch: shares torch's HIP runtime (same SONAME)
     import synth
@@ -337,13 +349,15 @@ def main():
     half = (args.ntaps - 1) // 2
     bits = args.bits or None
     flt = lcfir.Filter(taps, device=local, method=args.method)
+    if args.seg_len:
+        flt.set_fft_tuning(seg_len=args.seg_len)
     method = flt.method
 
     backend = TimedBackend(batch.DeviceBackend(flt, dev, lanes=args.lanes, own_streams=args.graph == "on"),
                            torch)
     runner = batch.BatchRunner(backend, rank, world, [n] * nfiles, nch, half, args.normalize,
                                args.peak_scope, batch.torch_allreduce_max(), lanes=args.lanes,
-                               fuse_normalize=not args.no_fuse_normalize)
+                               fuse_normalize=not args.no_fuse_normalize, force_exchange=args.force_exchange)
     # synthetic samples; configs 4/5 reuse two generated files to bound host time
     cache = {}
 
@@ -503,6 +517,7 @@ def main():
                 "workload": wl[args.config] + f", {args.ntaps}-tap low-cut",
                 "files": nfiles, "channels": nch, "samples_per_channel": n,
                 "ntaps": args.ntaps, "method": method,
+                "fft_plan": flt.fft_info if method == "fft" else None,
                 "parallelism": f"{world} rank(s), files sharded by batch.plan_shards",
                 "normalize": bool(args.normalize), "peak_scope": args.peak_scope,
                 "peak_exchange": runner.exchange,
@@ -557,6 +572,7 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
