@@ -1116,7 +1116,11 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
             const int c = 2 * (j + 512 * r);
             const float f0 = (float)a[r].x, f1 = (float)(-a[r].y);
             const bool ok = c >= cmin && (!kSym || c < cmax);
+#ifdef LCFIR_FFT_NOSTORE // timing-only tools builds: every store dropped by the range check
+            const int ob = (int)0x80000000;
+#else
             const int ob = ok ? (int)((off + c) * 4) : (int)0x80000000;
+#endif
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(f0), ys, ob, 0, kNtStore);
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(f1), ys, ob + 4, 0, kNtStore);
             pk = fmaxf(pk, ok ? fmaxf(fabsf(f0), fabsf(f1)) : 0.0f);

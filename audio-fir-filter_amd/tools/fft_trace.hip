@@ -50,7 +50,7 @@ int main(int argc, char **argv) {
     CK(hipMemcpy(dt, taps.data(), sizeof(double) * T, hipMemcpyHostToDevice));
     lcfir::FftPlan plan;
     std::string err;
-    if (!lcfir::fft_plan_build(plan, dt, T, nullptr, err)) {
+    if (!lcfir::fft_plan_build(plan, dt, T, lcfir::FftTuning{}, nullptr, err)) {
         std::fprintf(stderr, "plan: %s\n", err.c_str());
         return 1;
     }
