@@ -482,8 +482,10 @@ def main():
                     tj = json.load(f)
             except (OSError, ValueError):
                 continue
+            plan = flt.fft_info if method == "fft" else {}
             if tj.get("method") == method and tj.get("ntaps") == args.ntaps and \
-                    tj.get("samples_per_launch") == samples_per_launch:
+                    tj.get("samples_per_launch") == samples_per_launch and \
+                    tj.get("seg_len", 16384 if method == "fft" else None) == plan.get("seg_len"):
                 traffic = tj.get("hbm_bytes_per_launch")
                 f64_flops = tj.get("f64_flops_per_launch")
                 valu_insts = tj.get("valu_insts_per_launch")

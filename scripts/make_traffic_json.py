@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--ntaps", type=int, required=True)
     ap.add_argument("--samples-per-launch", type=float, required=True)
     ap.add_argument("--kernel", required=True)
+    ap.add_argument("--seg-len", type=int, default=16384, help="FFT segment length of the launch (0: direct)")
     a = ap.parse_args()
     s = json.load(open(a.summary))
     k = next(v for name, v in s.items() if a.kernel in name)
@@ -30,7 +31,7 @@ def main():
     alg = 8.0 * a.samples_per_launch
     out = {
         "method": a.method, "ntaps": a.ntaps, "samples_per_launch": a.samples_per_launch,
-        "kernel": a.kernel,
+        "kernel": a.kernel, "seg_len": a.seg_len if a.method == "fft" else None,
         "hbm_bytes_per_launch": read + write,
         "hbm_read_bytes_per_launch": read, "hbm_write_bytes_per_launch": write,
         "algorithmic_rw_bytes_per_launch": alg,
