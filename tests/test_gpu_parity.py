@@ -599,3 +599,28 @@ def test_fft_seg32_chunks_and_groups(lc, oracle_mod):
         for c in range(2):
             ref = oracle_mod.filter_channel(xs[c], taps, oracle_mod.MODE_LD)
             assert max_ulps(ys[c], ref) <= 1 and rms(ys[c], ref) <= RMS_TOL, (n, c)
+
+
+@pytest.mark.parametrize("ntaps,n,nch,want_L", [(12001, 3_000_000, 2, 32768), (19201, 48_000, 1, 16384),
+                                                (8001, 600_000, 8, 16384)])
+def test_fft_auto_seg_len(lc, oracle_mod, ntaps, n, nch, want_L):
+    """The automatic segment length (fir_fft.hpp fft_choose_seg_len), chosen at
+    the first call from its shape: a long filter on long channels takes the
+    L = 32 768 segment (12 001 taps: one partition instead of two), config 1's
+    short channel keeps L = 16 384, and 8 001 taps (even costs) stays at
+    16 384.  The product path as it runs by default, against the long-double
+    oracle at every edge sample and random positions, fused peaks."""
+    import synth
+    fs = 48000.0
+    taps = oracle_mod.design_lowcut(20.0, fs, ntaps)
+    x = synth.file_buffer(nch, n, fs, file=13, bits=24)
+    flt = lc.Filter(taps, method="fft")
+    y, pk = gpu_filter_channels(lc, flt, x)
+    assert flt.fft_info["seg_len"] == want_L
+    half = (ntaps - 1) // 2
+    for c in range(min(nch, 2)):
+        idx = _sample_positions(n, half, 1024, 1300 + c)
+        ref_ld, _ = oracle_mod.filter_points(x[c], taps, idx, oracle_mod.MODE_LD)
+        assert rms(y[c][idx], ref_ld) <= RMS_TOL, c
+        assert max_ulps(y[c][idx], ref_ld) <= 1, c
+    assert np.array_equal(pk, np.abs(y).max(axis=1))
