@@ -152,14 +152,13 @@ struct FftPlan {
 };
 
 // A filter runs in zero-phase form (kFftOutSym: real pair table, a cheaper
-// pair step) when it is one partition, half = (T-1)/2 is even (the output
-// pairs stay 8-byte aligned) and it is symmetric, h[k] = h[T-1-k], up to an
+// pair step) when it is one partition and it is symmetric, h[k] = h[T-1-k], up to an
 // antisymmetric part of at most 2^-50 of its l1 norm.  Dropping that part
 // changes any output by at most 2^-50 |h|_1 max|x| -- the size of the f64
 // FFT's own rounding error.  FftTuning::zero_phase = 0 turns the form off.
 inline bool fft_sym_eligible(const std::vector<double> &h, int parts, const FftTuning &tune) {
     const int T = (int)h.size();
-    if (!tune.zero_phase || parts != 1 || T < 3 || ((T - 1) / 2) % 2 != 0) return false;
+    if (!tune.zero_phase || parts != 1 || T < 3) return false;
     long double anti = 0.0L, norm = 0.0L;
     for (int k = 0; k < T; ++k) {
         anti += fabsl(((long double)h[(size_t)k] - (long double)h[(size_t)(T - 1 - k)]) * 0.5L);
@@ -1093,7 +1092,8 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     const __amdgpu_buffer_rsrc_t ys = __builtin_amdgcn_make_buffer_rsrc(
         yb, (short)0, (int)((p.end - p.start) * 4), 0x00020000);
     // valid outputs c in [cmin, cmax): [T-1, L) for the causal table, [half,
-    // L - half) for the zero-phase one (kSym: half even, fft_plan_build)
+    // L - half) for the zero-phase one (kSym, fft_plan_build; an odd half
+    // makes cmin odd)
     constexpr bool kSym = kOut == kFftOutSym;
     const int cmin = kSym ? p.half : p.ntaps - 1;
     const int cmax = kSym ? kFftL - p.half : kFftL;
@@ -1103,9 +1103,23 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
     const int64_t oend = p.end - p.start;
     float pk = 0.0f;
     if constexpr (kOut == kFftOutF32 || kSym) {
-    if (n0 >= p.start && n0 + B <= p.end) {
-        // every output of this unit is in [start, end): the pair (c, c+1) is
-        // valid iff cmin <= c < cmax (cmin, cmax and o are even), so both
+    if (kSym && (cmin & 1) && n0 >= p.start && n0 + B <= p.end) {
+        // the zero-phase form of an odd half: every output of this unit is
+        // in [start, end), but the ends of [cmin, cmax) split a pair
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int c = 2 * (j + 512 * r);
+            const float f0 = (float)a[r].x, f1 = (float)(-a[r].y);
+            const bool ok0 = c >= cmin && c < cmax, ok1 = c + 1 >= cmin && c + 1 < cmax;
+            const int ob = (int)((off + c) * 4);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(f0), ys, ok0 ? ob : (int)0x80000000, 0, kNtStore);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(f1), ys, ok1 ? ob + 4 : (int)0x80000000, 0,
+                                                  kNtStore);
+            pk = fmaxf(pk, fmaxf(ok0 ? fabsf(f0) : 0.0f, ok1 ? fabsf(f1) : 0.0f));
+        }
+    } else if (n0 >= p.start && n0 + B <= p.end) {
+        // every output of this unit is in [start, end) and cmin, cmax are
+        // even: the pair (c, c+1) is valid iff cmin <= c < cmax, so both
         // stores share one offset and may merge into a dwordx2.  (A resource
         // over the unit's B outputs, letting the range check drop the rest,
         // with a sign-bit mask for the peak removed the SGPR spills but

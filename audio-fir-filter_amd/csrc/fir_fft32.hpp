@@ -186,18 +186,22 @@ __device__ __forceinline__ float fft32_store_unit(const DirectParams &p, int ch,
 #endif
             }
         } else if (n0 >= p.start && n0 + B <= p.end) {
-            // every output of the unit is in [start, end): the pair (c, c+1) is
-            // valid iff cmin <= c < cmax; both stores share one offset
+            // every output of the unit is in [start, end); cmin is not a
+            // multiple of 4 (an odd one -- the zero-phase form of an odd half
+            // -- splits a pair at each end): each output of a pair checked on
+            // its own, both stores from one offset
 #pragma unroll
             for (int r = 0; r < 32; ++r) {
                 const int c = 2 * (j + 512 * r);
                 const double2 x = X(r);
                 const float f0 = (float)x.x, f1 = (float)(-x.y);
-                const bool ok = c >= cmin && (!kSym || c < cmax);
-                const int ob = ok ? (int)((off + c) * 4) : (int)0x80000000;
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(f0), ys, ob, 0, kFft32StoreAux);
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(f1), ys, ob + 4, 0, kFft32StoreAux);
-                pk = fmaxf(pk, ok ? fmaxf(fabsf(f0), fabsf(f1)) : 0.0f);
+                const bool ok0 = c >= cmin && (!kSym || c < cmax), ok1 = c + 1 >= cmin && (!kSym || c + 1 < cmax);
+                const int ob = (int)((off + c) * 4);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(f0), ys, ok0 ? ob : (int)0x80000000, 0,
+                                                      kFft32StoreAux);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(f1), ys, ok1 ? ob + 4 : (int)0x80000000, 0,
+                                                      kFft32StoreAux);
+                pk = fmaxf(pk, fmaxf(ok0 ? fabsf(f0) : 0.0f, ok1 ? fabsf(f1) : 0.0f));
             }
         } else {
 #pragma unroll

@@ -59,7 +59,9 @@ def parse():
     ap.add_argument("--fs", type=float, default=48000.0)
     ap.add_argument("--ntaps", type=int, default=4001)
     ap.add_argument("--seg-len", type=int, default=0, choices=[0, 16384, 32768],
-                    help="FFT segment length (0 = the library's choice by tap count)")
+                    help="FFT segment length (0 = the library's choice)")
+    ap.add_argument("--general-form", action="store_true",
+                    help="FFT: the general pair table even for linear-phase taps (zero-phase form off)")
     ap.add_argument("--bits", type=int, default=24, help="0 = float32 source")
     ap.add_argument("--normalize", action="store_true")
     ap.add_argument("--peak-scope", default="file", choices=["file", "global"])
@@ -349,8 +351,8 @@ def main():
     half = (args.ntaps - 1) // 2
     bits = args.bits or None
     flt = lcfir.Filter(taps, device=local, method=args.method)
-    if args.seg_len:
-        flt.set_fft_tuning(seg_len=args.seg_len)
+    if args.seg_len or args.general_form:
+        flt.set_fft_tuning(seg_len=args.seg_len, zero_phase=not args.general_form)
     method = flt.method
 
     backend = TimedBackend(batch.DeviceBackend(flt, dev, lanes=args.lanes, own_streams=args.graph == "on"),

@@ -42,7 +42,7 @@ def test_tables_emulated_segment(dump, tmp_path, seg_len, ntaps, sym):
     taps.astype(np.float64).tofile(tmp_path / "t.f64")
     subprocess.run([dump, str(tmp_path / "t.f64"), str(seg_len), "1", str(tmp_path / "tb")], check=True)
     tb = fm.load_tables(str(tmp_path / "tb"))
-    assert tb["L"] == seg_len and tb["parts"] == 1 and tb["sym"] == (sym and ((ntaps - 1) // 2) % 2 == 0)
+    assert tb["L"] == seg_len and tb["parts"] == 1 and tb["sym"] == sym
     rng = np.random.default_rng(ntaps)
     x = rng.uniform(-1, 1, seg_len)
     c = fm.emulate(x, tb)

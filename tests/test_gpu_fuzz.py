@@ -1,5 +1,5 @@
 """Seeded randomized GPU parity: random tap counts (odd, 1 .. 40 001; designed
-low-cuts, which run the FFT's zero-phase form when half is even, and random
+low-cuts, which run the FFT's zero-phase form (odd and even halves), and random
 taps, which run its general form), random channel counts and lengths (shorter
 than the filter included), random sub-ranges through the windowed entry point,
 both methods.  Every case against the oracle at sampled positions:
@@ -17,6 +17,8 @@ both methods.  Every case against the oracle at sampled positions:
 
 A second set fuzzes lcfir_filter_window_norm_dev (a previous file's normalize
 carried by the filter call) against the separate filter + normalize calls.
+About a third of the FFT cases of both sets force the L = 32 768 segment
+(_seg32), whose normalize is never fused (a separate pass).
 
 LCFIR_FUZZ_CASES / LCFIR_FUZZ_NORM_CASES / LCFIR_FUZZ_SEED0 widen or shift the
 seed range for a longer campaign (scripts/gpu_fuzz.sh); the defaults are the
@@ -47,6 +49,12 @@ def _max_ulps(a, b, floor=1e-12):
     return int(np.where(close, 0, np.abs(ia - ib)).max()) if a.size else 0
 
 
+def _seg32(seed):
+    """About a third of the FFT cases run the L = 32 768 segment (fir_fft32.hpp),
+    drawn from a stream of its own so the cases themselves stay as they were."""
+    return np.random.default_rng(90_000 + seed).random() < 0.35
+
+
 def _case(seed):
     rng = np.random.default_rng(1000 + seed)
     ntaps = int(rng.choice([1, 3, 5, 95, 97, 401, 1601, 4001, 4003, 8001, 10925, 19201, 40001]))
@@ -75,6 +83,8 @@ def test_random_case(oracle_mod, seed):
         x = np.rint(x * 2 ** (bits - 1)) / 2 ** (bits - 1)
     x = np.ascontiguousarray(x, np.float32)
     flt = lc.Filter(taps, method=method)
+    if method == "fft" and _seg32(seed):
+        flt.set_fft_tuning(seg_len=32768)
 
     dx = lc.DeviceBuffer.from_array(x)
     dy = lc.DeviceBuffer(x.nbytes)
@@ -179,6 +189,8 @@ def test_random_norm_case(oracle_mod, seed):
     x = np.ascontiguousarray(np.rint(rng.uniform(-0.9, 0.9, (nch, n)) * 2 ** 23) / 2 ** 23, np.float32)
     prev = (rng.standard_normal(count + offset) * 0.5).astype(np.float32)
     flt = lc.Filter(taps, method=method)
+    if method == "fft" and _seg32(seed):
+        flt.set_fft_tuning(seg_len=32768)
     dx = torch.from_numpy(x).cuda()
     res = []
     for fused in (False, True):

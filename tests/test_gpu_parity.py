@@ -478,9 +478,10 @@ def test_fft_channel_groups(lc, max_units):
 # ---- linear-phase filters: the zero-phase form (fir_fft.hpp fft_sym_eligible)
 @pytest.mark.parametrize("ntaps,perturb", [(4001, 0.0), (4001, 1e-9), (4003, 0.0), (801, 0.0)])
 def test_fft_zero_phase_form(lc, oracle_mod, ntaps, perturb):
-    """Symmetric taps with an even half run in zero-phase form (real pair
-    table, outputs c in [half, L - half)); odd halves and taps with a visible
-    antisymmetric part run the general table.  Every form against the
+    """Symmetric taps run in zero-phase form (real pair table, outputs c in
+    [half, L - half); an odd half, 4 003 taps, makes the range's ends odd and
+    takes the per-output store path); taps with a visible antisymmetric part
+    run the general table.  Every form against the
     long-double oracle, sub-ranges against whole channels (the shifted output
     window), and the zero-phase form against the general one on the same
     filter (lcfir_ctx_set_fft_tuning zero_phase 0)."""
@@ -501,7 +502,7 @@ def test_fft_zero_phase_form(lc, oracle_mod, ntaps, perturb):
     for start, end in [(1, n - 1), (half - 1, half + 12_385), (77_777, 77_778), (n - 13_000, n)]:
         check_window(lc, flt, x, y, start, end)
     # the general pair table on the same filter (zero-phase form off)
-    assert flt.fft_info["zero_phase"] == (perturb == 0.0 and ((ntaps - 1) // 2) % 2 == 0)
+    assert flt.fft_info["zero_phase"] == (perturb == 0.0)
     flt_g = lc.Filter(taps, method="fft")
     flt_g.set_fft_tuning(zero_phase=False)
     y_general, _ = gpu_filter_channels(lc, flt_g, x)
@@ -542,9 +543,9 @@ def test_staging_pool_cap_release_and_ctx_destroy(lc, oracle_mod):
 def test_fft_seg32_forms(lc, oracle_mod, ntaps, perturb):
     """The 32 768-sample segment (two 8192-point halves split by bin parity,
     park slab, radix-2 merge) forced by lcfir_ctx_set_fft_tuning, for the
-    zero-phase (4001, 8001, 19201 taps: one partition), general (4003: odd
-    half; 8001 with a visible antisymmetric part) and partitioned (38401,
-    100001) forms: against the long-double oracle at every edge sample and
+    zero-phase (4001, 8001, 19201 taps: one partition; 4003: odd half, the
+    per-output store path), general (8001 with a visible antisymmetric part)
+    and partitioned (38401, 100001) forms: against the long-double oracle at every edge sample and
     random positions, within 1 ulp of the 16 384-sample segment, windowed calls
     bit-identical to the whole channel, the reference's thread hand-off
     bit-identical, peaks fused."""
@@ -558,7 +559,7 @@ def test_fft_seg32_forms(lc, oracle_mod, ntaps, perturb):
     flt.set_fft_tuning(seg_len=32768)
     info = flt.fft_info
     assert info["seg_len"] == 32768
-    assert info["zero_phase"] == (perturb == 0.0 and ntaps in (4001, 8001, 19201))
+    assert info["zero_phase"] == (perturb == 0.0 and ntaps in (4001, 4003, 8001, 19201))
     y, pk = gpu_filter_channels(lc, flt, x)
     half = (ntaps - 1) // 2
     for c in range(2):
