@@ -243,6 +243,10 @@ class BatchRunner:
         """Output handle of shard `index` in buffer set `which` of `lane`."""
         return self._outs[lane][which][index]
 
+    def output_buffer_set(self, lane: int, which: int = 0):
+        """Every shard's output handle in buffer set `which` of `lane`."""
+        return list(self._outs[lane][which])
+
     def _slot(self, sh: Shard) -> Optional[int]:
         return None if self.scope == "global" else sh.file
 
@@ -352,11 +356,15 @@ class DeviceBackend(Backend):
         self.dirty = set()
         self.graph_waiters = set()
 
-    def set_lane(self, lane):
-        s = self.streams[lane]
+    def _after_graph(self, lane):
+        # the lane's work of the last one-graph replay ran on lane 0's stream
         if lane in self.graph_waiters:
             self.graph_waiters.discard(lane)
-            s.wait_stream(self.streams[0])
+            self.streams[lane].wait_stream(self.streams[0])
+
+    def set_lane(self, lane):
+        s = self.streams[lane]
+        self._after_graph(lane)
         self.dirty.add(lane)
         self.stream, self.sp = s, s.cuda_stream
         # torch-side work of the step (the RCCL peak exchange) follows the lane
@@ -367,6 +375,7 @@ class DeviceBackend(Backend):
             for o in self.streams:
                 if o is not s:
                     s.wait_stream(o)
+        self.graph_waiters.clear()  # every lane now follows lane 0's stream too
 
     def retain(self, handle, lane):
         # allocated on the caller's stream, written/read on another lane's
@@ -378,7 +387,9 @@ class DeviceBackend(Backend):
 
     def publish(self, lane):
         # the current stream (lane 0's after a step) and the allocation stream
-        # both wait for the lane
+        # both wait for the lane (and, after a one-graph replay, for the
+        # graph, which ran the lane's steps on lane 0's stream)
+        self._after_graph(lane)
         cur = self.torch.cuda.current_stream(self.dev)
         cur.wait_stream(self.streams[lane])
         if self.alloc_stream != cur:

@@ -476,6 +476,69 @@ def test_graph_replay_then_eager_steps(tt, oracle_mod, lanes):
     torch.cuda.set_stream(torch.cuda.default_stream(dev))
 
 
+@pytest.mark.parametrize("lanes", [2, 3])
+def test_graph_replay_results_on_allocation_stream(tt, oracle_mod, lanes):
+    """results() straight after a one-graph replay, read on the stream the
+    runner's buffers were allocated on (not lane 0's, where the graph ran):
+    publish() must order that stream behind the graph, which ran every lane's
+    steps on lane 0's stream (the lazy lane waits, DeviceBackend._after_graph).
+    The latest lane's outputs are poisoned and lane 0's stream spins before the
+    replay, so a read that does not wait for the graph sees NaN -- where the
+    two streams sit on different hardware queues: HIP multiplexes streams onto
+    GPU_MAX_HW_QUEUES (4 here), and two streams on one queue are ordered anyway
+    (on the one-GPU box the unfixed publish() passed this test for that reason).
+    Correct by construction; kept as the regression check for boxes that map
+    the streams apart."""
+    torch, lc = tt
+    import batch
+    import synth
+    taps = oracle_mod.design_lowcut(20.0, 48000.0, 4001)
+    half = (taps.size - 1) // 2
+    files = [synth.file_buffer(2, 4_000_000, 48000.0, file=20 + f, bits=24) for f in range(2)]
+    flt = lc.Filter(taps, method="fft")
+    dev = torch.device("cuda", 0)
+    # a stream of its own: the legacy default stream would order itself
+    # behind every other stream and hide a missing wait
+    alloc = torch.cuda.Stream(dev)
+    nf = [f.shape[1] for f in files]
+
+    def fresh():
+        torch.cuda.set_stream(alloc)
+        be = batch.DeviceBackend(flt, dev, lanes=lanes, own_streams=True)
+        r = batch.BatchRunner(be, 0, 1, nf, 2, half, False, "file", lanes=lanes)
+        r.prepare(lambda f, lo, hi: files[f][:, lo:hi])
+        return be, r
+
+    be, r = fresh()
+    g = batch.GraphedSteps(r, be)
+    torch.cuda.synchronize(dev)
+    with torch.cuda.stream(be.streams[0]):
+        for y in r.output_buffer_set(lanes - 1):
+            y.fill_(float("nan"))
+        torch.cuda._sleep(40_000_000)  # ~20 ms of spinning ahead of the replay on lane 0's stream
+    g.replay()
+    res = r.results()
+    with torch.cuda.stream(alloc):
+        # a device-side read on that stream (a copy to host memory could be
+        # ordered by the copy engine instead)
+        snap = [y.clone() for _, y in res]
+    torch.cuda.synchronize(dev)
+    got = [z.cpu().numpy() for z in snap]
+    r.close()
+    torch.cuda.set_stream(alloc)
+    total = sum(r._steps)
+    be, r = fresh()
+    for _ in range(total):
+        r.step()
+    want = [y.cpu().numpy() for _, y in r.results()]
+    r.close()
+    torch.cuda.set_stream(alloc)
+    torch.cuda.set_stream(torch.cuda.default_stream(dev))
+    for a, b in zip(want, got):
+        assert not np.isnan(b).any()
+        assert np.array_equal(a, b)
+
+
 @pytest.fixture(scope="module")
 def nccl_world1(tt):
     """A world-size-1 RCCL process group on this GPU (torch.distributed
