@@ -540,7 +540,8 @@ def main():
                 "frac_step_note": "4 B x samples per step per GPU / ms_per_step / 8 TB/s (whole step: "
                                   "launch gaps, collective, normalize passes, lane overlap included)",
                 "traffic": traffic,
-                "kernel": "fir_direct_f64_kernel" if method == "direct" else "fir_fft_f64_kernel",
+                "kernel": "fir_direct_f64_kernel" if method == "direct" else
+                          ("fir_fft32_f64_kernel" if flt.fft_info["seg_len"] == 32768 else "fir_fft_f64_kernel"),
                 "kernel_ms": round(kern_ms, 6),
                 "kernel_ms_note": f"exclusive: {kern_launches} launches of the filter alone on one "
                                   f"stream right after the pre-roll (HIP events on that stream)",

@@ -3,6 +3,7 @@
 # the f64 VALU counts, each its own rocprofv3 --pmc pass, then
 # scripts/pmc_summary.py + scripts/make_traffic_json.py -> profiles/traffic_<tag>.json.
 # usage: bash scripts/gpu_traffic.sh <tag> <ntaps> <samples_per_launch> [bench args...]
+# (SEG_LEN=32768 KERNEL=fir_fft32_f64_kernel for the long segment)
 set -u -o pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 TAG=$1 NTAPS=$2 SPL=$3; shift 3
@@ -21,4 +22,4 @@ done
 cd "$ROOT"
 python scripts/pmc_summary.py "$OUT" --json "$OUT/summary.json" > /dev/null &&
 python scripts/make_traffic_json.py "$OUT/summary.json" "$ROOT/gpurun_out/traffic_$TAG.json" --method fft \
-    --ntaps "$NTAPS" --samples-per-launch "$SPL" --kernel fir_fft_f64_kernel
+    --ntaps "$NTAPS" --samples-per-launch "$SPL" --kernel "${KERNEL:-fir_fft_f64_kernel}" --seg-len "${SEG_LEN:-16384}"
