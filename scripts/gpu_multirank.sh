@@ -26,4 +26,8 @@ run mr_c2_n2 2 --steps 10 --warmup 2 --preroll-s 0.5
 run mr_c4_n2 2 --config 4 --steps 3 --warmup 1 --preroll-s 0.5
 run mr_c5_n2 2 --config 5 --steps 3 --warmup 1 --preroll-s 0.5
 run mr_c4f1_n2 2 --config 4 --files 1 --steps 3 --warmup 1 --preroll-s 0.5
+# round 3: config 5 at one file per rank (the N = 8 shape: exchange every step,
+# each rescale deferred into the lane's next launch), and 8 ranks of config 2
+run mr_c5f2_n2 2 --config 5 --files 2 --steps 4 --warmup 1 --preroll-s 0.5
+run mr_c2_n8 8 --steps 6 --warmup 2 --preroll-s 0.5
 echo "== done"
