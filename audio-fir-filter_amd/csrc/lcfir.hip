@@ -123,8 +123,11 @@ int resolve_method(lcfir_ctx *ctx) {
 }
 
 // The FFT plan, built at the first use: its segment length (unless tuned) is
-// chosen for that call's shape, outputs per channel x nch (0: unknown),
-// lcfir::fft_choose_seg_len
+// chosen for that call's shape, the channel length x nch (0: unknown),
+// lcfir::fft_choose_seg_len.  The channel's length, not the call's range:
+// every range of a channel -- the reference's per-thread chunks, the ranks of
+// a split file -- then gets the same plan, hence the same segment grid and
+// the same bytes, whichever call comes first.
 int ensure_fft(lcfir_ctx *ctx, int64_t outputs = 0, int nch = 1) {
     std::lock_guard<std::mutex> lk(ctx->fft_mu);
     if (ctx->fft.ready) return LCFIR_OK;
@@ -194,7 +197,7 @@ int launch_normalize(float *d_y, int64_t stride, int32_t nch, int64_t n, const u
 // track_stream: remember s for lcfir_ctx_destroy's wait (false for the
 // staging streams of lcfir_apply_range, which synchronises its stream before
 // returning and may destroy it later, lcfir_staging_release).
-int run_filter(lcfir_ctx *ctx, lcfir::DirectParams p, int nch, hipStream_t s,
+int run_filter(lcfir_ctx *ctx, lcfir::DirectParams p, int nch, hipStream_t s, int64_t chan_n,
                const lcfir::FftNrm *nrm = nullptr, bool track_stream = true) {
     p.taps = ctx->d_taps;
     p.ntaps = ctx->ntaps;
@@ -202,7 +205,7 @@ int run_filter(lcfir_ctx *ctx, lcfir::DirectParams p, int nch, hipStream_t s,
     if (track_stream) note_stream(ctx, s);
     const int m = resolve_method(ctx);
     if (m == LCFIR_METHOD_FFT) {
-        int rc = ensure_fft(ctx, p.end - p.start, nch);
+        int rc = ensure_fft(ctx, chan_n, nch);
         if (rc) return rc;
         std::string err;
         // per-stream scratch: the L = 32768 kernel's park slabs, then the
@@ -480,7 +483,7 @@ static int range_window(lcfir_ctx *ctx, int64_t n, int64_t start, int64_t end, i
     lo = start - ctx->half;
     hi = end + ctx->half;
     if (resolve_method(ctx) == LCFIR_METHOD_FFT) {
-        const int rc = ensure_fft(ctx, end - start, 1);
+        const int rc = ensure_fft(ctx, n, 1);
         if (rc) return rc;
         lcfir::fft_window(ctx->fft, ctx->half, start, end, lo, hi);
     }
@@ -542,7 +545,7 @@ int lcfir_apply_range(lcfir_ctx *ctx, const float *x, int64_t n, float *y, int64
         p.start = start;
         p.end = end;
         p.peak = nullptr;
-        rc = run_filter(ctx, p, 1, st->stream, nullptr, /*track_stream=*/false);
+        rc = run_filter(ctx, p, 1, st->stream, n, nullptr, /*track_stream=*/false);
     }
     if (!rc) {
         if (hipMemcpyAsync(y + start, st->d_y, sizeof(float) * (size_t)(end - start),
@@ -607,7 +610,7 @@ int lcfir_apply_range_dev(lcfir_ctx *ctx, const float *d_x, int64_t n, float *d_
     p.y_lo = 0;
     p.start = start;
     p.end = end;
-    return run_filter(ctx, p, 1, reinterpret_cast<hipStream_t>(stream));
+    return run_filter(ctx, p, 1, reinterpret_cast<hipStream_t>(stream), n);
 }
 
 int lcfir_filter_channels_dev(lcfir_ctx *ctx, const float *d_x, int64_t x_stride, int32_t nch,
@@ -635,7 +638,7 @@ int lcfir_filter_channels_dev(lcfir_ctx *ctx, const float *d_x, int64_t x_stride
     p.end = n;
     p.peak = d_peak ? peak_bits(d_peak) : nullptr;
     p.peak_stride = 1;
-    return run_filter(ctx, p, nch, reinterpret_cast<hipStream_t>(stream));
+    return run_filter(ctx, p, nch, reinterpret_cast<hipStream_t>(stream), n);
 }
 
 static int filter_window(lcfir_ctx *ctx, const float *d_xw, int64_t x_lo, int64_t x_hi, int64_t x_stride,
@@ -673,7 +676,7 @@ static int filter_window(lcfir_ctx *ctx, const float *d_xw, int64_t x_lo, int64_
     p.end = end;
     p.peak = d_peak ? peak_bits(d_peak) : nullptr;
     p.peak_stride = peak_stride;
-    return run_filter(ctx, p, nch, reinterpret_cast<hipStream_t>(stream), nrm);
+    return run_filter(ctx, p, nch, reinterpret_cast<hipStream_t>(stream), n, nrm);
 }
 
 int lcfir_filter_window_dev(lcfir_ctx *ctx, const float *d_xw, int64_t x_lo, int64_t x_hi,

@@ -85,10 +85,12 @@ int lcfir_ctx_fft_info(lcfir_ctx *ctx, int32_t *seg_len, int32_t *parts, int32_t
 /* Explicit FFT-method choices for this ctx (the library reads no environment
  * variables).  seg_len: 0 = automatic, or 16384 / 32768.  Automatic picks,
  * once per ctx when its plan is built (the first filter or window call), the
- * length with the lower estimated time for that call's shape: tap partitions
- * x persistent-grid rounds x the measured unit cost (a 32768-sample unit
- * costs 2.9 16384-sample ones); fft_info / window calls without a channel
- * count assume one channel.  zero_phase: 1 = linear-phase filters run in zero-phase form (the
+ * length with the lower estimated time for that call's channel length n and
+ * channel count: tap partitions x persistent-grid rounds x the measured unit
+ * cost (a 32768-sample unit costs 2.9 16384-sample ones).  The channel's
+ * length, not the call's range, so every range of a channel (threads, ranks
+ * of a split file) gets the same plan; window calls assume one channel,
+ * fft_info (no length) the per-output cost.  zero_phase: 1 = linear-phase filters run in zero-phase form (the
  * default), 0 = always the general pair table; chunk: outputs per launch
  * chunk (0 = 2^28, else >= 4096); max_units: segments x channels per launch
  * (0 = 2^31 - 1).  Every setting gives outputs within 1 f32 ulp of every

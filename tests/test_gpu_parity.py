@@ -625,3 +625,28 @@ def test_fft_auto_seg_len(lc, oracle_mod, ntaps, n, nch, want_L):
         assert rms(y[c][idx], ref_ld) <= RMS_TOL, c
         assert max_ulps(y[c][idx], ref_ld) <= 1, c
     assert np.array_equal(pk, np.abs(y).max(axis=1))
+
+
+def test_fft_auto_seg_len_follows_the_channel(lc, oracle_mod):
+    """The automatic choice depends on the channel's length, not on the first
+    call's range: a ctx whose first call is a 50 000-output range of a
+    3 M-sample channel (the reference's per-thread chunk, a rank's share of a
+    split file) picks the same segment length as one whose first call is the
+    whole channel, so the range's bytes equal the whole-channel call's."""
+    import synth
+    taps = oracle_mod.design_lowcut(20.0, 48000.0, 12001)
+    n = 3_000_000
+    x = np.ascontiguousarray(synth.file_buffer(1, n, 48000.0, file=14, bits=24)[0])
+    whole = lc.Filter(taps, method="fft")
+    y, _ = gpu_filter_channels(lc, whole, x[None, :])
+    part = lc.Filter(taps, method="fft")
+    dx = lc.DeviceBuffer.from_array(x)
+    dy = lc.DeviceBuffer.from_array(np.zeros(n, np.float32))
+    start, end = 1_234_567, 1_284_567
+    part.apply_range_dev(dx, n, dy, start, end)
+    lc.sync()
+    yr = dy.download(n)
+    dx.free()
+    dy.free()
+    assert whole.fft_info["seg_len"] == part.fft_info["seg_len"] == 32768
+    assert np.array_equal(yr[start:end], y[0][start:end])
