@@ -1,5 +1,5 @@
 #!/bin/bash
-# GPU-box run of BASELINE.json configs 1, 3, 4 and 5 at N = 1 (bench lines) plus a
+# GPU-box run of BASELINE.json configs 1-5 at N = 1 (bench lines) plus a
 # rocprofv3 kernel-stats pass per config.  Every GPU step has its own time
 # limit; the first failure ends the script.
 # usage (from the repo root, on the GPU box): bash scripts/gpu_configs.sh [tag]
@@ -17,8 +17,9 @@ step() { # name timeout cmd...
     tail -2 "$OUT/$name.log" | cut -c1-3000
     if [ $rc -ne 0 ]; then echo "!! $name failed rc=$rc"; tail -40 "$OUT/$name.log"; exit $rc; fi
 }
-step bench_c1 300 python bench.py --config 1
-step bench_c3 300 python bench.py --config 3
+step bench_c2 300 python bench.py --steps 20 --warmup 5
+step bench_c1 300 python bench.py --config 1 --steps 20 --warmup 5
+step bench_c3 300 python bench.py --config 3 --steps 20 --warmup 5
 step bench_c4 600 python bench.py --config 4 --steps 20 --warmup 3
 step bench_c5 600 python bench.py --config 5 --steps 20 --warmup 3 --no-cpu-baseline
 step bench_c5g 600 python bench.py --config 5 --peak-scope global --steps 20 --warmup 3 --no-cpu-baseline
