@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--files", type=int, default=4)
     ap.add_argument("--minutes", type=float, default=10.0)
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "e2e.json"))
+    ap.add_argument("--readers", type=int, default=0, help="lowcut --readers (0: the tool's default)")
+    ap.add_argument("--devices", default=None, help="lowcut --devices")
     a = ap.parse_args()
     rate, nch = 48000, 2
     n = int(a.minutes * 60 * rate)
@@ -47,17 +49,21 @@ def main():
         exe = os.path.join(ROOT, "audio-fir-filter_amd", "lowcut")
         out_dir = os.path.join(work, "out")
         t0 = time.time()
-        r = subprocess.run([exe, "--timing", "-f", "20", "-s", "48", *paths, out_dir],
+        extra = ["--readers", str(a.readers)] if a.readers else []
+        extra += ["--devices", a.devices] if a.devices else []
+        r = subprocess.run([exe, "--timing", "-f", "20", "-s", "48", *extra, *paths, out_dir],
                            capture_output=True, text=True, timeout=1200)
         wall = time.time() - t0
         if r.returncode != 0:
             sys.exit(f"lowcut failed: {r.stderr}")
-        m = re.search(r"timing total: (\d+) file\(s\), ([\d.]+) s, ([\d.]+) Msamples/s", r.stdout)
+        m = re.search(r"timing total: (\d+) file\(s\), .*?, ([\d.]+) s, ([\d.]+) Msamples/s", r.stdout)
         per_file = re.findall(r"timing (\S+): read ([\d.]+) s, gpu ([\d.]+) s .*write ([\d.]+) s",
                               r.stdout)
         res = {
             "what": "lowcut end to end (disk + pinned host + PCIe + GPU), pipelined across files",
             "files": a.files, "minutes_per_file": a.minutes, "format": "stereo 48 kHz s24le WAVE",
+            "readers": a.readers, "devices": a.devices,
+            "summary_line": next((l for l in r.stdout.splitlines() if l.startswith("timing total")), None),
             "ntaps": 4001, "samples": a.files * nch * n,
             "tool_seconds": float(m.group(2)), "msamples_per_s": float(m.group(3)),
             "process_wall_seconds": wall, "input_generation_seconds": gen_s,

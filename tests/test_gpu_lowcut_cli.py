@@ -291,8 +291,9 @@ def test_batch_over_device_stages(tmp_path, oracle_mod):
     file per GPU).  On the one-GPU box the stages share device 0 ("0,0,0":
     three stages, each with its own contexts, streams and slots): every output
     byte-identical to the single-stage run, written in input order, checked
-    against the oracle; with a missing input in the middle the files before it
-    are written and the ones after it are not (main.cp:131-146)."""
+    against the oracle; the same with files read by parallel reader threads
+    (--readers); with a missing input in the middle (four readers) the files
+    before it are written and the ones after it are not (main.cp:131-146)."""
     specs = [(48000, 2, "s24le", "wav", 60000), (44100, 1, "s16le", "wav", 20001),
              (96000, 2, "f32le", "wav", 40000), (48000, 1, "s24be", "aif", 33333),
              (48000, 3, "s32le", "wav", 25000), (44100, 2, "s16be", "aif", 12345),
@@ -309,13 +310,21 @@ def test_batch_over_device_stages(tmp_path, oracle_mod):
     names = [line.split(": ", 1)[1] for line in out.splitlines() if line.startswith("Processing file:")]
     assert names == [s[0].name for s in srcs]
     assert "3 GPU stage(s)" in out
+    # files read by three threads in parallel: same bytes, same order
+    par = tmp_path / "par"
+    out = lowcut("-n", "-f", 25, "-s", 50, "--devices", "0,0", "--readers", "3", "--timing",
+                 *[s[0] for s in srcs], par)
+    names = [line.split(": ", 1)[1] for line in out.splitlines() if line.startswith("Processing file:")]
+    assert names == [s[0].name for s in srcs]
+    assert "3 reader(s)" in out
     for p, x, rate, fmt in srcs:
         assert open(one / p.name, "rb").read() == open(three / p.name, "rb").read(), p.name
+        assert open(one / p.name, "rb").read() == open(par / p.name, "rb").read(), p.name
         xq = pcm_ref.np_decode(pcm_ref.np_encode(x, fmt), fmt, x.shape[0])
         check_file(oracle_mod, p, three / p.name, xq, rate, fmt, 25, 50, True)
     stop = tmp_path / "stop"
-    args = ["-f", 20, "-s", 48, "--devices", "0,0", *[s[0] for s in srcs[:3]], tmp_path / "missing.wav",
-            *[s[0] for s in srcs[3:]], stop]
+    args = ["-f", 20, "-s", 48, "--devices", "0,0", "--readers", "4", *[s[0] for s in srcs[:3]],
+            tmp_path / "missing.wav", *[s[0] for s in srcs[3:]], stop]
     r = subprocess.run([LOWCUT, *map(str, args)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 1 and "not found" in r.stderr
     assert all((stop / s[0].name).exists() for s in srcs[:3])

@@ -152,3 +152,11 @@ def test_plan_deals_files_round_robin(tmp_path):
         assert r.returncode == 1 and "--devices" in r.stderr
     r = run("--plan", *files, outdir)
     assert r.returncode == 1 and "--plan needs --devices" in r.stderr
+
+
+def test_readers_option_validation(tmp_path):
+    """--readers takes 1..64 reader threads (files read in parallel, written in
+    input order); anything else is a usage error."""
+    for bad in ("0", "65", "x", "-1"):
+        r = run("--readers", bad, tmp_path / "a.wav", tmp_path / "b.wav")
+        assert r.returncode == 1 and "--readers" in r.stderr, bad
