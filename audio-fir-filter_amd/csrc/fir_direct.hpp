@@ -9,12 +9,14 @@
 // Mapping (output-stationary, no cross-lane reduction):
 //   * a workgroup owns BO = NT*R consecutive outputs of one channel;
 //   * lane `tid` owns the R consecutive outputs n0 + tid*R + [0, R);
-//   * taps are processed in stages of <= tc taps: each stage stages the taps
-//     h[c, c+kc) and the f64-converted sample window x[n0 - half + c, +BO+kc)
-//     in LDS (f32 -> f64 conversion happens once per staged sample, not per
-//     tap), then every lane slides a 2R-sample register window over its part
-//     of the LDS window: per R taps it reads R samples (ds_read_b64) and R
-//     wave-uniform taps (LDS broadcast) and issues R*R v_fma_f64.
+//   * taps are processed in stages of <= TC taps (rounded up to R with zero
+//     taps): each stage stages the
+//     f64-converted sample window x[n0 - half + c, +BO+kc) in LDS (f32 -> f64
+//     conversion happens once per staged sample, not per tap), then every
+//     lane slides a 2R-sample register window over its part of the LDS
+//     window: per R taps it reads R samples (ds_read_b64) and R wave-uniform
+//     taps (scalar loads into SGPRs, h[c, c+kc) from the zero-padded device
+//     copy) and issues R*R v_fma_f64.
 //   * the LDS sample window is padded by one double every R doubles, so the
 //     lane-strided ds_read_b64 of 32 lanes hit 64 distinct banks.
 //   * accumulation order per output is k = 0, 1, ..., T-1, one fused
@@ -43,7 +45,6 @@ struct DirectParams {
     int32_t half;
     int64_t start, end; // output range (global indices)
     int64_t seg0;       // FFT only: first output of the launch's first segment (<= start; fft_launch_group)
-    int32_t tc;         // taps per LDS stage (multiple of 2R)
     unsigned *peak;     // max|y| as float bits (nullable): channel c -> peak[c * peak_stride]
     int64_t peak_stride;
     double *y64;        // partitioned FFT only: f64 partial sums, element 0 = output `start`
@@ -51,9 +52,14 @@ struct DirectParams {
     double2 *park;      // L = 32768 FFT only: the workgroups' park slabs (fir_fft32.hpp)
 };
 
+// Taps are read through the constant address space: wave-uniform scalar
+// loads into SGPRs (v_fma_f64 takes one SGPR operand), which leaves the
+// VGPRs to the accumulators and the sample window.
+typedef const __attribute__((address_space(4))) double *ctap_ptr;
+
 template <int R>
 __device__ __forceinline__ void fma_block(double (&acc)[R], const double (&wlo)[R],
-                                          const double (&whi)[R], const double *__restrict__ t) {
+                                          const double (&whi)[R], ctap_ptr t) {
 #pragma unroll
     for (int u = 0; u < R; ++u) {
         const double h = t[u];
@@ -65,79 +71,161 @@ __device__ __forceinline__ void fma_block(double (&acc)[R], const double (&wlo)[
     }
 }
 
-template <int R, int NT>
-__global__ __launch_bounds__(NT) void fir_direct_f64_kernel(DirectParams p) {
+// One tile = BO outputs of one channel.  The grid is capped at what the chip
+// holds at once (launch_direct) and every workgroup walks its channel's tiles
+// with stride gridDim.x, so the fused peak leaves a workgroup as ONE atomic
+// per launch: one per wave per tile (57 600 same-address atomics for a
+// 28.8 M-sample stereo launch) held a 15-tap filter at 0.67 ms, ~9x its HBM
+// time.  Per tile:
+//   * staging issues all of a lane's window loads before the first
+//     conversion (KW range-checked buffer loads in flight, not one round trip
+//     per element);
+//   * outputs leave through LDS: lane tid's R results go to a padded row, and
+//     the wave then stores consecutive floats (one 256-B run per instruction
+//     instead of 64 lanes 64 B apart).
+template <int R, int NT, int TC>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void fir_direct_f64_kernel(DirectParams p) {
     extern __shared__ double lds[];
+    __shared__ float pk_lds[NT / 64];
     constexpr int BO = NT * R;
+    constexpr int KW = (BO + TC + NT - 1) / NT; // window elements per lane, max
     const int ch = blockIdx.y;
-    const int tid = threadIdx.x;
     const float *__restrict__ x = p.x + (int64_t)ch * p.x_stride;
-    const int64_t n0 = p.start + (int64_t)blockIdx.x * BO;
-
-    double *sh_t = lds;
-    double *sh_x = lds + p.tc;
-
-    double acc[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) acc[r] = 0.0;
-
-    for (int c = 0; c < p.ntaps; c += p.tc) {
-        // taps in this stage, rounded up to 2R (zero taps beyond T)
-        int kc = p.ntaps - c;
-        if (kc > p.tc) kc = p.tc;
-        kc = (kc + 2 * R - 1) / (2 * R) * (2 * R);
-        for (int i = tid; i < kc; i += NT) {
-            const int k = c + i;
-            sh_t[i] = (k < p.ntaps) ? p.taps[k] : 0.0;
-        }
-        const int win = BO + kc;
-        const int64_t g0 = n0 - p.half + c;
-        for (int i = tid; i < win; i += NT) {
-            const int64_t g = g0 + i;
-            const float v = (g >= p.x_lo && g < p.x_hi) ? x[g - p.x_lo] : 0.0f;
-            sh_x[i + i / R] = (double)v;
-        }
-        __syncthreads();
-
-        const double *__restrict__ wp = sh_x + tid * (R + 1);
-        double wa[R], wb[R];
-#pragma unroll
-        for (int j = 0; j < R; ++j) wa[j] = wp[j];
-        for (int k = 0; k < kc; k += 2 * R) {
-            const int blk = k / R; // window block index (R samples per block, R+1 with pad)
-#pragma unroll
-            for (int j = 0; j < R; ++j) wb[j] = wp[(blk + 1) * (R + 1) + j];
-            fma_block<R>(acc, wa, wb, sh_t + k);
-#pragma unroll
-            for (int j = 0; j < R; ++j) wa[j] = wp[(blk + 2) * (R + 1) + j];
-            fma_block<R>(acc, wb, wa, sh_t + k + R);
-        }
-        __syncthreads();
-    }
-
-    float m = 0.0f;
     float *__restrict__ y = p.y + (int64_t)ch * p.y_stride;
-    const int64_t gb = n0 + (int64_t)tid * R;
+    const ctap_ptr taps = (ctap_ptr)p.taps; // zero-padded to a multiple of TC (lcfir_ctx_create)
+    double *sh_x = lds;
+    float *sh_y = reinterpret_cast<float *>(lds); // reused after the last stage
+    const int64_t ntiles = (p.end - p.start + BO - 1) / BO;
+    float m = 0.0f;
+
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t n0 = p.start + tile * BO;
+        // laundered per tile: the per-element offsets below are recomputed,
+        // not hoisted out of the tile loop into ~80 spilled registers
+        unsigned tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        double acc[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int64_t g = gb + r;
-        if (g < p.end) {
-            const float v = (float)acc[r];
-            y[g - p.y_lo] = v;
-            m = fmaxf(m, fabsf(v));
+        for (int r = 0; r < R; ++r) acc[r] = 0.0;
+
+        for (int c = 0; c < p.ntaps; c += TC) {
+            // taps in this stage, rounded up to R (zero taps beyond T): a
+            // 15-tap filter issues 16 fmas per output, not 32
+            int kc = p.ntaps - c;
+            if (kc > TC) kc = TC;
+            kc = (kc + R - 1) / R * R;
+            const int win = BO + kc;
+            const int64_t g0 = n0 - p.half + c;
+            // raw buffer loads through a resource over the part of the window
+            // that holds data, [lo, hi): element i >= lead reads offset
+            // 4 (i - lead), offsets past the resource read 0 (the zero padding
+            // of FilterCore.h's shortened edge sums), and elements before the
+            // data (i < lead) take an offset far past it -- a compare and a
+            // select per load, no reliance on negative offsets wrapping.  One
+            // offset register per load, KW loads in flight, 32-bit offsets for
+            // any channel length.
+            const int64_t lo = g0 > p.x_lo ? g0 : p.x_lo;
+            const int64_t hi = g0 + win < p.x_hi ? g0 + win : p.x_hi;
+            const bool any = hi > lo;
+            const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<float *>(x) + (any ? lo - p.x_lo : 0), (short)0, any ? (int)(4 * (hi - lo)) : 0,
+                0x00020000);
+            const int lead = (int)(lo - g0 < win ? lo - g0 : win);
+            int ts = (int)tid; // laundered per stage: per-j offsets are not hoisted
+            asm volatile("" : "+v"(ts));
+            float v[KW];
+#pragma unroll
+            for (int j = 0; j < KW; ++j) {
+                const int i = ts + NT * j;
+                const int o = i >= lead ? 4 * (i - lead) : 0x7ffffff0;
+                v[j] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, o, 0, 0));
+            }
+            // window element i = tid + j NT sits at i + i / R (one pad double
+            // per R): a per-lane base plus a constant per j, since NT % R == 0
+            double *__restrict__ xs = sh_x + (tid + tid / R);
+#pragma unroll
+            for (int j = 0; j < BO / NT; ++j) xs[j * (NT + NT / R)] = (double)v[j];
+#pragma unroll
+            for (int j = BO / NT; j < KW; ++j)
+                if (tid + j * NT < win) xs[j * (NT + NT / R)] = (double)v[j];
+            __syncthreads();
+
+            const double *__restrict__ wp = sh_x + tid * (R + 1);
+            double wa[R], wb[R];
+#pragma unroll
+            for (int j = 0; j < R; ++j) wa[j] = wp[j];
+            int k = 0;
+#pragma unroll 1
+            for (; k + 2 * R <= kc; k += 2 * R) {
+                const int blk = k / R; // window block index (R samples per block, R+1 with pad)
+#pragma unroll
+                for (int j = 0; j < R; ++j) wb[j] = wp[(blk + 1) * (R + 1) + j];
+                fma_block<R>(acc, wa, wb, taps + c + k);
+#pragma unroll
+                for (int j = 0; j < R; ++j) wa[j] = wp[(blk + 2) * (R + 1) + j];
+                fma_block<R>(acc, wb, wa, taps + c + k + R);
+            }
+            if (k < kc) { // an odd number of R-tap blocks: the last one
+                const int blk = k / R;
+#pragma unroll
+                for (int j = 0; j < R; ++j) wb[j] = wp[(blk + 1) * (R + 1) + j];
+                fma_block<R>(acc, wa, wb, taps + c + k);
+            }
+            __syncthreads();
         }
+
+        // lane tid's outputs -> LDS row tid (R + 1 floats, conflict-free), then
+        // output i = tid + j*NT of the tile leaves from row i / R
+#pragma unroll
+        for (int r = 0; r < R; ++r) sh_y[tid * (R + 1) + r] = (float)acc[r];
+        __syncthreads();
+        const int64_t rem = p.end - n0; // outputs left in the range, > 0
+        float *__restrict__ yt = y + (n0 - p.y_lo) + tid;
+        // output i = tid + j NT is row i / R = tid / R + j NT / R, column tid % R
+        const float *__restrict__ ys = sh_y + (tid / R) * (R + 1) + tid % R;
+        // no select of min(rem, BO): hipcc (ROCm 7.2) compiled that one into an
+        // s_cselect on a stale SCC, so a range's last, partial tile stored all
+        // BO outputs (into the next channel)
+        if (rem >= BO) {
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                const float v = ys[j * (NT / R) * (R + 1)];
+                yt[j * NT] = v;
+                m = fmaxf(m, fabsf(v));
+            }
+        } else {
+            const int cnt = (int)rem;
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                if ((int)tid + j * NT < cnt) {
+                    const float v = ys[j * (NT / R) * (R + 1)];
+                    yt[j * NT] = v;
+                    m = fmaxf(m, fabsf(v));
+                }
+            }
+        }
+        __syncthreads(); // the next tile's staging overwrites sh_y
     }
+
     if (p.peak) {
+        const int tid = threadIdx.x;
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
-        if ((tid & 63) == 0) atomicMax(p.peak + ch * p.peak_stride, __float_as_uint(m));
+        if ((tid & 63) == 0) pk_lds[tid >> 6] = m;
+        __syncthreads();
+        if (tid == 0) {
+            float pk = pk_lds[0];
+#pragma unroll
+            for (int w = 1; w < NT / 64; ++w) pk = fmaxf(pk, pk_lds[w]);
+            atomicMax(p.peak + ch * p.peak_stride, __float_as_uint(pk));
+        }
     }
 }
 
-// LDS bytes a launch of fir_direct_f64_kernel<R, NT> needs for stage size tc.
-template <int R, int NT>
-constexpr size_t direct_lds_bytes(int tc) {
-    return sizeof(double) * ((size_t)tc + (size_t)(NT * R + tc) / R * (R + 1) + (R + 1));
+// LDS bytes a launch of fir_direct_f64_kernel<R, NT, TC> needs.
+template <int R, int NT, int TC>
+constexpr size_t direct_lds_bytes() {
+    return sizeof(double) * ((size_t)(NT * R + TC) / R * (R + 1) + (R + 1));
 }
 
 } // namespace lcfir

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -96,23 +97,39 @@ struct DeviceGuard {
 constexpr int kDirR = 16;   // outputs per lane
 constexpr int kDirNT = 256; // threads per workgroup (4 waves)
 constexpr int kDirTC = 256; // taps per LDS stage -> 39 KB LDS -> 4 workgroups / CU
+constexpr int kDirWgPerCu = 4;
+
+// Compute units of the current device (cached per device id).
+int device_cus() {
+    static std::atomic<int> cache[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    int c = cache[dev].load(std::memory_order_relaxed);
+    if (c > 0) return c;
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0)
+        c = 256;
+    cache[dev].store(c, std::memory_order_relaxed);
+    return c;
+}
 
 int launch_direct(lcfir::DirectParams p, int nch, hipStream_t s) {
     const int64_t count = p.end - p.start;
     if (count <= 0 || nch <= 0) return LCFIR_OK;
     constexpr int BO = kDirR * kDirNT;
-    p.tc = kDirTC;
-    const int64_t gx = (count + BO - 1) / BO;
-    if (gx > 0x7fffffff || nch > 65535) return fail(LCFIR_EINVAL, "range too large for one launch");
-    const size_t lds = lcfir::direct_lds_bytes<kDirR, kDirNT>(kDirTC);
+    if (nch > 65535) return fail(LCFIR_EINVAL, "range too large for one launch");
+    // tile-looping grid: what the chip holds at once (kDirWgPerCu per CU,
+    // split over the channels), fir_direct.hpp
+    const int64_t tiles = (count + BO - 1) / BO;
+    const int64_t cap = std::max<int64_t>(1, (int64_t)device_cus() * kDirWgPerCu / nch);
+    const int64_t gx = std::min(tiles, cap);
+    constexpr size_t lds = lcfir::direct_lds_bytes<kDirR, kDirNT, kDirTC>();
+    auto *kern = &lcfir::fir_direct_f64_kernel<kDirR, kDirNT, kDirTC>;
     static std::once_flag attr_once;
     std::call_once(attr_once, [&] {
-        (void)hipFuncSetAttribute(
-            reinterpret_cast<const void *>(&lcfir::fir_direct_f64_kernel<kDirR, kDirNT>),
-            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     });
-    hipLaunchKernelGGL((lcfir::fir_direct_f64_kernel<kDirR, kDirNT>), dim3((unsigned)gx, nch),
-                       dim3(kDirNT), lds, s, p);
+    hipLaunchKernelGGL(kern, dim3((unsigned)gx, nch), dim3(kDirNT), lds, s, p);
     LCFIR_HIP(hipGetLastError());
     return LCFIR_OK;
 }
@@ -372,10 +389,13 @@ int lcfir_ctx_create(int device, const double *taps, int32_t ntaps, lcfir_ctx **
         return fail(LCFIR_EDEVICE, "stream creation failed");
     }
     int rc = LCFIR_OK;
-    if (hipMallocAsync(reinterpret_cast<void **>(&ctx->d_taps), sizeof(double) * (size_t)ntaps, ctx->own) !=
-        hipSuccess)
+    // zero-padded to a whole number of direct-kernel stages: the kernel reads
+    // the taps of a stage rounded up to 2R without a bound check
+    const size_t padded = (size_t)(ntaps + kDirTC - 1) / kDirTC * kDirTC;
+    if (hipMallocAsync(reinterpret_cast<void **>(&ctx->d_taps), sizeof(double) * padded, ctx->own) != hipSuccess)
         rc = fail(LCFIR_ENOMEM, "hipMallocAsync for %d taps failed", ntaps);
-    else if (hipMemcpyAsync(ctx->d_taps, taps, sizeof(double) * (size_t)ntaps, hipMemcpyHostToDevice,
+    else if (hipMemsetAsync(ctx->d_taps, 0, sizeof(double) * padded, ctx->own) != hipSuccess ||
+             hipMemcpyAsync(ctx->d_taps, taps, sizeof(double) * (size_t)ntaps, hipMemcpyHostToDevice,
                             ctx->own) != hipSuccess ||
              hipStreamSynchronize(ctx->own) != hipSuccess)
         rc = fail(LCFIR_EDEVICE, "tap upload failed");

@@ -64,7 +64,7 @@ def _case(seed):
     # the FFT is exact only to ~1e-16, so taps with few significant bits can
     # land outputs on f32 rounding ties (test_gpu_parity.TIE_PRONE); AUTO runs
     # such short filters with the direct method, and so does this test
-    method = "direct" if ntaps < 96 or (ntaps <= 2001 and rng.random() < 0.4) else "fft"
+    method = "direct" if ntaps < 64 or (ntaps <= 2001 and rng.random() < 0.4) else "fft"
     designed = rng.random() < 0.6
     return rng, ntaps, nch, max(1, n), method, designed
 

@@ -650,3 +650,42 @@ def test_fft_auto_seg_len_follows_the_channel(lc, oracle_mod):
     dy.free()
     assert whole.fft_info["seg_len"] == part.fft_info["seg_len"] == 32768
     assert np.array_equal(yr[start:end], y[0][start:end])
+
+
+# ---- the loads' zero padding at every window alignment
+@pytest.mark.parametrize("method,ntaps,seg_len,zero_phase", [
+    ("direct", 15, 0, True), ("direct", 97, 0, True), ("direct", 801, 0, True), ("direct", 4003, 0, True),
+    ("fft", 4001, 16384, True), ("fft", 4003, 16384, True), ("fft", 4003, 16384, False),
+    ("fft", 4005, 32768, True), ("fft", 4003, 32768, False), ("fft", 19203, 16384, True)])
+def test_edge_outputs_every_window_alignment(lc, oracle_mod, method, ntaps, seg_len, zero_phase):
+    """Outputs next to a window edge: the whole channel's first and last T + 256
+    outputs, and windowed calls whose window [x_lo, x_hi) starts d = 0..3
+    samples before the first sample the outputs need (and ends d after the
+    last).  Samples outside a window read as zeros through the loads'
+    range-checked buffer resources ("negative" offsets are out of range), so
+    every alignment of the window against the kernels' load offsets -- the
+    sample pair straddling the window start, lanes whose first loads fall
+    before it and later ones after -- is checked against the oracle: bit for
+    bit (direct, strict fma order) or <= 1 ulp (FFT)."""
+    n = 120_001
+    rng = np.random.default_rng(ntaps + seg_len)
+    x = (rng.integers(-2**23, 2**23, size=(1, n)) / 2.0**23).astype(np.float32)
+    taps = oracle_mod.design_lowcut(20.0, 48000.0, ntaps)
+    half = (ntaps - 1) // 2
+    flt = lc.Filter(taps, method=method)
+    if method == "fft":
+        flt.set_fft_tuning(seg_len=seg_len, zero_phase=zero_phase)
+    span = ntaps + 256  # every output whose taps reach past a window edge, and more
+    cases = [(0, span, 0, n), (n - span, n, 0, n)]
+    for d in range(4):
+        s0 = 30_000 + 7 * d
+        cases.append((s0, s0 + span, s0 - half - d, s0 + span + half + d))
+    for start, end, x_lo, x_hi in cases:
+        yw = gpu_filter_window(lc, flt, x, start, end, x_lo, x_hi)[0]
+        idx = np.arange(start, end)
+        if method == "direct":
+            ref, _ = oracle_mod.filter_points(x[0], taps, idx, oracle_mod.MODE_FMA)
+            assert np.array_equal(yw, ref), (start, x_lo)
+        else:
+            ref, _ = oracle_mod.filter_points(x[0], taps, idx, oracle_mod.MODE_LD)
+            assert max_ulps(yw, ref) <= 1 and rms(yw, ref) <= RMS_TOL, (start, x_lo)
