@@ -351,23 +351,30 @@ def test_config3_full_size(lc, oracle_mod, method):
 
 
 @pytest.mark.slow
-def test_fft_channel_beyond_2gib(lc, oracle_mod):
+@pytest.mark.parametrize("method,ntaps", [("fft", 4001), ("direct", 31)])
+def test_channel_beyond_2gib(lc, oracle_mod, method, ntaps):
     """One channel of 2^29 + 4097 samples (2.15 GB of f32): past the 32-bit
-    byte range of the FFT kernel's buffer offsets, so fir_fft.hpp must split
-    the launch (fft_chunk, 2^28 outputs).  Checked against the long-double
-    oracle at both edges, around both chunk seams and at random positions;
-    the fused peak against the full output."""
+    byte range of buffer offsets.  The FFT splits the launch (fir_fft.hpp
+    fft_chunk, 2^28 outputs); the direct kernel rebases its load resource at
+    every stage and walks 64-bit tile indices.  Checked against the oracle at
+    both edges, around both 2^28 / 2^29 seams and at random positions (long
+    double for the FFT, bit for bit against the strict fma chain for the
+    direct form); the fused peak against the full output."""
     n = (1 << 29) + 4097
     rng = np.random.default_rng(29)
     x = (rng.standard_normal(n, dtype=np.float32) * np.float32(0.2))[None, :]
-    taps = oracle_mod.design_lowcut(20.0, 48000.0, 4001)
-    flt = lc.Filter(taps, method="fft")
+    taps = oracle_mod.design_lowcut(20.0, 48000.0, ntaps)
+    flt = lc.Filter(taps, method=method)
     y, pk = gpu_filter_channels(lc, flt, x)
     seams = np.r_[[(1 << 28) + d for d in range(-40, 40)], [(1 << 29) + d for d in range(-40, 40)]]
-    idx = np.unique(np.r_[_sample_positions(n, 2000, 2048, 29), seams])
-    ref_ld, _ = oracle_mod.filter_points(x[0], taps, idx, oracle_mod.MODE_LD)
-    assert rms(y[0][idx], ref_ld) <= RMS_TOL
-    assert max_ulps(y[0][idx], ref_ld) <= 1
+    idx = np.unique(np.r_[_sample_positions(n, ntaps // 2, 2048, 29), seams])
+    if method == "direct":
+        ref, _ = oracle_mod.filter_points(x[0], taps, idx, oracle_mod.MODE_FMA)
+        assert np.array_equal(y[0][idx], ref)
+    else:
+        ref_ld, _ = oracle_mod.filter_points(x[0], taps, idx, oracle_mod.MODE_LD)
+        assert rms(y[0][idx], ref_ld) <= RMS_TOL
+        assert max_ulps(y[0][idx], ref_ld) <= 1
     assert pk[0] == np.abs(y[0]).max()
     assert np.isfinite(y[0]).all()
 
