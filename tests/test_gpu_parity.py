@@ -676,7 +676,9 @@ def test_edge_outputs_every_window_alignment(lc, oracle_mod, method, ntaps, seg_
     bit (direct, strict fma order) or <= 1 ulp (FFT)."""
     n = 120_001
     rng = np.random.default_rng(ntaps + seg_len)
-    x = (rng.integers(-2**23, 2**23, size=(1, n)) / 2.0**23).astype(np.float32)
+    # two channels: a tile or unit that stored past its range would land in
+    # the next channel's outputs
+    x = (rng.integers(-2**23, 2**23, size=(2, n)) / 2.0**23).astype(np.float32)
     taps = oracle_mod.design_lowcut(20.0, 48000.0, ntaps)
     half = (ntaps - 1) // 2
     flt = lc.Filter(taps, method=method)
@@ -688,11 +690,12 @@ def test_edge_outputs_every_window_alignment(lc, oracle_mod, method, ntaps, seg_
         s0 = 30_000 + 7 * d
         cases.append((s0, s0 + span, s0 - half - d, s0 + span + half + d))
     for start, end, x_lo, x_hi in cases:
-        yw = gpu_filter_window(lc, flt, x, start, end, x_lo, x_hi)[0]
+        yw = gpu_filter_window(lc, flt, x, start, end, x_lo, x_hi)
         idx = np.arange(start, end)
-        if method == "direct":
-            ref, _ = oracle_mod.filter_points(x[0], taps, idx, oracle_mod.MODE_FMA)
-            assert np.array_equal(yw, ref), (start, x_lo)
-        else:
-            ref, _ = oracle_mod.filter_points(x[0], taps, idx, oracle_mod.MODE_LD)
-            assert max_ulps(yw, ref) <= 1 and rms(yw, ref) <= RMS_TOL, (start, x_lo)
+        for c in range(2):
+            if method == "direct":
+                ref, _ = oracle_mod.filter_points(x[c], taps, idx, oracle_mod.MODE_FMA)
+                assert np.array_equal(yw[c], ref), (c, start, x_lo)
+            else:
+                ref, _ = oracle_mod.filter_points(x[c], taps, idx, oracle_mod.MODE_LD)
+                assert max_ulps(yw[c], ref) <= 1 and rms(yw[c], ref) <= RMS_TOL, (c, start, x_lo)
