@@ -71,20 +71,59 @@ __device__ __forceinline__ void fma_block(double (&acc)[R], const double (&wlo)[
     }
 }
 
+// The window of one stage: x[g0, g0 + win) of the channel into v, element
+// i = ts + NT j in v[j].  Raw buffer loads through a resource over the part of
+// the window that holds data, [lo, hi): element i >= lead reads offset
+// 4 (i - lead), offsets past the resource read 0 (the zero padding of
+// FilterCore.h's shortened edge sums), and elements before the data (i < lead)
+// take an offset far past it -- a compare and a select per load, no reliance on
+// negative offsets wrapping.  One offset register per load, all KW loads in
+// flight at once, 32-bit offsets for any channel length.
+template <int NT, int KW>
+__device__ __forceinline__ void direct_load_window(const DirectParams &p, const float *x, int64_t g0, int win,
+                                                   int ts, float (&v)[KW]) {
+    const int64_t lo = g0 > p.x_lo ? g0 : p.x_lo;
+    const int64_t hi = g0 + win < p.x_hi ? g0 + win : p.x_hi;
+    const bool any = hi > lo;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float *>(x) + (any ? lo - p.x_lo : 0), (short)0, any ? (int)(4 * (hi - lo)) : 0, 0x00020000);
+    const int lead = (int)(lo - g0 < win ? lo - g0 : win);
+#pragma unroll
+    for (int j = 0; j < KW; ++j) {
+        const int i = ts + NT * j;
+        const int o = i >= lead ? 4 * (i - lead) : 0x7ffffff0;
+        v[j] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, o, 0, 0));
+    }
+}
+
+// taps in stage c, rounded up to R (zero taps beyond T): a 15-tap filter
+// issues 16 fmas per output, not 32
+template <int R, int TC>
+__device__ __forceinline__ int direct_stage_taps(int ntaps, int c) {
+    int kc = ntaps - c;
+    if (kc > TC) kc = TC;
+    return (kc + R - 1) / R * R;
+}
+
 // One tile = BO outputs of one channel.  The grid is capped at what the chip
 // holds at once (launch_direct) and every workgroup walks its channel's tiles
 // with stride gridDim.x, so the fused peak leaves a workgroup as ONE atomic
 // per launch: one per wave per tile (57 600 same-address atomics for a
 // 28.8 M-sample stereo launch) held a 15-tap filter at 0.67 ms, ~9x its HBM
-// time.  Per tile:
-//   * staging issues all of a lane's window loads before the first
-//     conversion (KW range-checked buffer loads in flight, not one round trip
-//     per element);
+// time.  Per stage (tile, c):
+//   * the window's KW loads per lane were issued during the previous stage's
+//     fmas (direct_load_window), so HBM latency overlaps the arithmetic; the
+//     stage converts them into LDS;
 //   * outputs leave through LDS: lane tid's R results go to a padded row, and
 //     the wave then stores consecutive floats (one 256-B run per instruction
 //     instead of 64 lanes 64 B apart).
+// 3 waves per SIMD: 147 VGPRs hold the next stage's window beside the
+// accumulators and the register window (4 spilled 25); the launch caps the
+// grid at 3 workgroups per CU to match (lcfir.hip kDirWgPerCu)
+constexpr int kDirectWavesPerSimd = 3;
+
 template <int R, int NT, int TC>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void fir_direct_f64_kernel(DirectParams p) {
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(kDirectWavesPerSimd))) void fir_direct_f64_kernel(DirectParams p) {
     extern __shared__ double lds[];
     __shared__ float pk_lds[NT / 64];
     constexpr int BO = NT * R;
@@ -98,6 +137,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void fi
     const int64_t ntiles = (p.end - p.start + BO - 1) / BO;
     float m = 0.0f;
 
+    float v[KW]; // the next stage's window, in flight
+    if ((int64_t)blockIdx.x < ntiles)
+        direct_load_window<NT, KW>(p, x, p.start + (int64_t)blockIdx.x * BO - p.half, BO + direct_stage_taps<R, TC>(p.ntaps, 0),
+                                   (int)threadIdx.x, v);
+
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t n0 = p.start + tile * BO;
         // laundered per tile: the per-element offsets below are recomputed,
@@ -109,37 +153,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void fi
         for (int r = 0; r < R; ++r) acc[r] = 0.0;
 
         for (int c = 0; c < p.ntaps; c += TC) {
-            // taps in this stage, rounded up to R (zero taps beyond T): a
-            // 15-tap filter issues 16 fmas per output, not 32
-            int kc = p.ntaps - c;
-            if (kc > TC) kc = TC;
-            kc = (kc + R - 1) / R * R;
+            const int kc = direct_stage_taps<R, TC>(p.ntaps, c);
             const int win = BO + kc;
-            const int64_t g0 = n0 - p.half + c;
-            // raw buffer loads through a resource over the part of the window
-            // that holds data, [lo, hi): element i >= lead reads offset
-            // 4 (i - lead), offsets past the resource read 0 (the zero padding
-            // of FilterCore.h's shortened edge sums), and elements before the
-            // data (i < lead) take an offset far past it -- a compare and a
-            // select per load, no reliance on negative offsets wrapping.  One
-            // offset register per load, KW loads in flight, 32-bit offsets for
-            // any channel length.
-            const int64_t lo = g0 > p.x_lo ? g0 : p.x_lo;
-            const int64_t hi = g0 + win < p.x_hi ? g0 + win : p.x_hi;
-            const bool any = hi > lo;
-            const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-                const_cast<float *>(x) + (any ? lo - p.x_lo : 0), (short)0, any ? (int)(4 * (hi - lo)) : 0,
-                0x00020000);
-            const int lead = (int)(lo - g0 < win ? lo - g0 : win);
-            int ts = (int)tid; // laundered per stage: per-j offsets are not hoisted
-            asm volatile("" : "+v"(ts));
-            float v[KW];
-#pragma unroll
-            for (int j = 0; j < KW; ++j) {
-                const int i = ts + NT * j;
-                const int o = i >= lead ? 4 * (i - lead) : 0x7ffffff0;
-                v[j] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, o, 0, 0));
-            }
             // window element i = tid + j NT sits at i + i / R (one pad double
             // per R): a per-lane base plus a constant per j, since NT % R == 0
             double *__restrict__ xs = sh_x + (tid + tid / R);
@@ -149,6 +164,22 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void fi
             for (int j = BO / NT; j < KW; ++j)
                 if (tid + j * NT < win) xs[j * (NT + NT / R)] = (double)v[j];
             __syncthreads();
+
+            // the next stage's window: (tile, c + TC), else the next tile's first
+            {
+                int64_t nt = tile;
+                int nc = c + TC;
+                if (nc >= p.ntaps) {
+                    nc = 0;
+                    nt = tile + gridDim.x;
+                }
+                if (nt < ntiles) {
+                    int ts = (int)tid; // laundered per stage: per-j offsets are not hoisted
+                    asm volatile("" : "+v"(ts));
+                    direct_load_window<NT, KW>(p, x, p.start + nt * BO - p.half + nc,
+                                               BO + direct_stage_taps<R, TC>(p.ntaps, nc), ts, v);
+                }
+            }
 
             const double *__restrict__ wp = sh_x + tid * (R + 1);
             double wa[R], wb[R];

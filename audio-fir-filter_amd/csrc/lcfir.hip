@@ -97,7 +97,7 @@ struct DeviceGuard {
 constexpr int kDirR = 16;   // outputs per lane
 constexpr int kDirNT = 256; // threads per workgroup (4 waves)
 constexpr int kDirTC = 256; // taps per LDS stage -> 39 KB LDS -> 4 workgroups / CU
-constexpr int kDirWgPerCu = 4;
+constexpr int kDirWgPerCu = lcfir::kDirectWavesPerSimd; // one wave per SIMD per workgroup
 
 // Compute units of the current device (cached per device id).
 int device_cus() {
