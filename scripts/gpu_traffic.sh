@@ -3,7 +3,8 @@
 # the f64 VALU counts, each its own rocprofv3 --pmc pass, then
 # scripts/pmc_summary.py + scripts/make_traffic_json.py -> profiles/traffic_<tag>.json.
 # usage: bash scripts/gpu_traffic.sh <tag> <ntaps> <samples_per_launch> [bench args...]
-# (SEG_LEN=32768 KERNEL=fir_fft32_f64_kernel for the long segment)
+# (SEG_LEN=32768 KERNEL=fir_fft32_f64_kernel for the long segment;
+#  METHOD=direct KERNEL=fir_direct_f64_kernel with --method direct)
 set -u -o pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 TAG=$1 NTAPS=$2 SPL=$3; shift 3
@@ -21,5 +22,5 @@ for c in FETCH_SIZE WRITE_SIZE "SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VAL
 done
 cd "$ROOT"
 python scripts/pmc_summary.py "$OUT" --json "$OUT/summary.json" > /dev/null &&
-python scripts/make_traffic_json.py "$OUT/summary.json" "$ROOT/gpurun_out/traffic_$TAG.json" --method fft \
+python scripts/make_traffic_json.py "$OUT/summary.json" "$ROOT/gpurun_out/traffic_$TAG.json" --method "${METHOD:-fft}" \
     --ntaps "$NTAPS" --samples-per-launch "$SPL" --kernel "${KERNEL:-fir_fft_f64_kernel}" --seg-len "${SEG_LEN:-16384}"
