@@ -47,7 +47,7 @@ typedef enum lcfir_status {
 
 /* How the convolution is evaluated.  All methods meet the same parity bar. */
 typedef enum lcfir_method {
-    LCFIR_METHOD_AUTO = 0,   /* fastest method for the tap count */
+    LCFIR_METHOD_AUTO = 0,   /* fastest method for the tap count: direct below 64 taps, else FFT */
     LCFIR_METHOD_DIRECT = 1, /* strict-order f64 FMA chain per output (bit-exact vs the
                                 oracle's ORACLE_FMA restatement) */
     LCFIR_METHOD_FFT = 2     /* f64 overlap-save FFT convolution, any T up to 2^20 taps (longer
