@@ -94,6 +94,20 @@ def test_formats_fft_path(tmp_path, oracle_mod, container, fmt, comp):
     check_file(oracle_mod, src, dst, xq, 48000, fmt, 20, 48, False)
 
 
+@pytest.mark.parametrize("slope,method,ntaps", [(4000, "direct", 49), (2000, "fft", 97)])
+def test_short_filter_method_choice(tmp_path, oracle_mod, slope, method, ntaps):
+    """A wide slope gives a short kernel: AUTO runs the direct kernel below
+    64 taps (-s 4000 at 48 kHz: 49 taps) and the FFT from 64 (-s 2000: 97).
+    Same file contract and oracle as every other case."""
+    x = tone(2, 50_001, 48000)
+    src, dst = tmp_path / "in.wav", tmp_path / "out.wav"
+    pcm_ref.write_wave(src, x, 48000, "s24le")
+    xq = pcm_ref.np_decode(pcm_ref.np_encode(x, "s24le"), "s24le", 2)
+    out = lowcut("-v", "-f", 1000, "-s", slope, src, dst)
+    assert f"{ntaps} taps ({method})" in out
+    check_file(oracle_mod, src, dst, xq, 48000, "s24le", 1000, slope, False)
+
+
 @pytest.mark.parametrize("normalize,loud", [(True, False), (False, True)])
 def test_normalize_rule(tmp_path, oracle_mod, normalize, loud):
     """ProcessFile.cp:92-101: rescale iff the file's peak > 1 or -n."""
