@@ -96,8 +96,10 @@ struct DeviceGuard {
 // ---- direct kernel configuration ---------------------------------------
 constexpr int kDirR = 16;   // outputs per lane
 constexpr int kDirNT = 256; // threads per workgroup (4 waves)
-constexpr int kDirTC = 256; // taps per LDS stage -> 39 KB LDS -> 4 workgroups / CU
-constexpr int kDirWgPerCu = lcfir::kDirectWavesPerSimd; // one wave per SIMD per workgroup
+constexpr int kDirTC = 256; // taps per LDS stage -> 37 KB LDS per workgroup
+// workgroups per CU the grid is capped at: the VGPR budget's waves per SIMD
+// (each workgroup puts one wave on every SIMD)
+constexpr int kDirWgPerCu = lcfir::kDirectWavesPerSimd;
 
 // Compute units of the current device (cached per device id).
 int device_cus() {
