@@ -170,8 +170,8 @@ inline bool fft_sym_eligible(const std::vector<double> &h, int parts, const FftT
 inline bool fft_supported(int ntaps) { return ntaps >= 1 && ntaps <= kFftMaxTaps; }
 // AUTO's choice: the direct kernel (bit-exact, strict fma order) up to 63
 // taps, where it is as fast as the FFT or faster (config-2 shape, r03:
-// 629 / 506 / 438 / 359 Gs/s at 15 / 31 / 47 / 63 taps vs the FFT's flat
-// ~360), the FFT above (368 vs 316 at 79 taps, 358 vs 274 at 95)
+// 658 / 562 / 451 / 375 Gs/s at 15 / 31 / 47 / 63 taps vs the FFT's flat
+// ~360), the FFT above (365 vs 317 at 79 taps, 364 vs 275 at 95)
 inline bool fft_preferred(int ntaps) { return ntaps >= 64 && fft_supported(ntaps); }
 
 // taps per partition when `parts` partitions share `ntaps` taps (odd: the
