@@ -699,3 +699,29 @@ def test_edge_outputs_every_window_alignment(lc, oracle_mod, method, ntaps, seg_
             else:
                 ref, _ = oracle_mod.filter_points(x[c], taps, idx, oracle_mod.MODE_LD)
                 assert max_ulps(yw[c], ref) <= 1 and rms(yw[c], ref) <= RMS_TOL, (c, start, x_lo)
+
+
+@pytest.mark.parametrize("method,ntaps", [("direct", 31), ("direct", 801), ("fft", 4001)])
+def test_many_channels(lc, oracle_mod, method, ntaps):
+    """300 channels in one call: more channels than the direct kernel's grid
+    holds workgroups per channel (launch_direct caps it at 3 per CU split over
+    the channels, so each channel gets one or two), and the FFT's channel x
+    segment unit grid.  A sample of channels against the oracle (bit for bit
+    for the direct form), every channel's fused peak against its output, and
+    the channels' independence: a channel of zeros stays zeros."""
+    nch, n = 300, 9_001
+    rng = np.random.default_rng(300 + ntaps)
+    x = (rng.integers(-2**23, 2**23, size=(nch, n)) / 2.0**23).astype(np.float32)
+    x[17] = 0.0
+    taps = oracle_mod.design_lowcut(20.0, 48000.0, ntaps)
+    flt = lc.Filter(taps, method=method)
+    y, pk = gpu_filter_channels(lc, flt, x)
+    assert not y[17].any() and pk[17] == 0.0
+    for c in [0, 1, 150, 298, 299]:
+        if method == "direct":
+            ref = oracle_mod.filter_channel(x[c], taps, oracle_mod.MODE_FMA)
+            assert np.array_equal(y[c], ref), c
+        else:
+            ref = oracle_mod.filter_channel(x[c], taps, oracle_mod.MODE_LD)
+            assert max_ulps(y[c], ref) <= 1 and rms(y[c], ref) <= RMS_TOL, c
+    assert np.array_equal(pk, np.abs(y).max(axis=1))
