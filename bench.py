@@ -494,6 +494,15 @@ def main():
                 break
         # The f64 kernels are bound by VALU issue, not HBM: the launch's PMC
         # instruction counts (profiles/traffic_latest.json) over the live kernel time.
+        # The resource whose floor is higher for this launch.  The direct form
+        # issues one fma per tap rounded up to 16 (fir_direct.hpp) against 8 B
+        # of HBM read + write per sample: below ~40 taps HBM is the floor.  The
+        # FFT is bound by its f64 issue and LDS-exchange latency (DESIGN s4.2).
+        if method == "direct":
+            t16 = (args.ntaps + 15) // 16 * 16
+            binding = "hbm" if 8.0 / (HBM_PEAK_GBPS * 1e9) > 2.0 * t16 / (FP64_PEAK_TFLOPS * 1e12) else "fp64-valu"
+        else:
+            binding = "fp64-valu"
         simds = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
         fp64_tflops = f64_flops / kern_s / 1e12 if f64_flops else None
         valu_frac = valu_insts * VALU_NS_PER_INST * 1e-9 / (simds * kern_s) if valu_insts else None
@@ -555,7 +564,7 @@ def main():
                 # None when the timed steps were graph replays (no per-launch events)
                 "overlapped_kernel_ms": round(overlapped_ms, 6) if launches else None,
                 "bytes_per_unit": 4,
-                "binding": "fp64-valu",
+                "binding": binding,
                 "direct_equiv_fp64_tflops": round(direct_tflops, 3),
                 "fp64_frac": round(direct_tflops / FP64_PEAK_TFLOPS, 4) if method == "direct"
                 else (round(fp64_tflops / FP64_PEAK_TFLOPS, 4) if fp64_tflops else None),
