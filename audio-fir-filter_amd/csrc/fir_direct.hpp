@@ -7,16 +7,16 @@
 // for n in [start, end) of every channel in the grid's y dimension.
 //
 // Mapping (output-stationary, no cross-lane reduction):
-//   * a workgroup owns BO = NT*R consecutive outputs of one channel;
+//   * a tile is BO = NT*R consecutive outputs of one channel; a workgroup
+//     walks its channel's tiles (the grid is capped, fir_direct_f64_kernel);
 //   * lane `tid` owns the R consecutive outputs n0 + tid*R + [0, R);
 //   * taps are processed in stages of <= TC taps (rounded up to R with zero
-//     taps): each stage stages the
-//     f64-converted sample window x[n0 - half + c, +BO+kc) in LDS (f32 -> f64
-//     conversion happens once per staged sample, not per tap), then every
-//     lane slides a 2R-sample register window over its part of the LDS
-//     window: per R taps it reads R samples (ds_read_b64) and R wave-uniform
-//     taps (scalar loads into SGPRs, h[c, c+kc) from the zero-padded device
-//     copy) and issues R*R v_fma_f64.
+//     taps): each stage converts the sample window x[n0 - half + c, +BO+kc)
+//     to f64 into LDS (once per staged sample, not per tap), then every lane
+//     slides a 2R-sample register window over its part of the LDS window: per
+//     R taps it reads R samples (ds_read_b64) and R wave-uniform taps (scalar
+//     loads into SGPRs, h[c, c+kc) from the zero-padded device copy) and
+//     issues R*R v_fma_f64;
 //   * the LDS sample window is padded by one double every R doubles, so the
 //     lane-strided ds_read_b64 of 32 lanes hit 64 distinct banks.
 //   * accumulation order per output is k = 0, 1, ..., T-1, one fused
