@@ -725,3 +725,45 @@ def test_many_channels(lc, oracle_mod, method, ntaps):
             ref = oracle_mod.filter_channel(x[c], taps, oracle_mod.MODE_LD)
             assert max_ulps(y[c], ref) <= 1 and rms(y[c], ref) <= RMS_TOL, c
     assert np.array_equal(pk, np.abs(y).max(axis=1))
+
+
+@pytest.mark.parametrize("method,ntaps,seg_len", [("direct", 31, 0), ("direct", 801, 0), ("fft", 4001, 16384),
+                                                 ("fft", 4003, 16384), ("fft", 8001, 32768)])
+def test_padded_channel_strides(lc, oracle_mod, method, ntaps, seg_len):
+    """lcfir_filter_window_dev with channel strides wider than the window and
+    the outputs (x_stride = window + 13, y_stride = count + 7, odd on
+    purpose): the outputs byte-identical to the packed layout's, the padding
+    of y never written (a sentinel survives), per-channel peaks equal."""
+    nch, n = 3, 70_001
+    rng = np.random.default_rng(ntaps + 7)
+    x = (rng.integers(-2**23, 2**23, size=(nch, n)) / 2.0**23).astype(np.float32)
+    taps = oracle_mod.design_lowcut(20.0, 48000.0, ntaps)
+    flt = lc.Filter(taps, method=method)
+    if method == "fft":
+        flt.set_fft_tuning(seg_len=seg_len)
+    start, end = 12_345, 61_000
+    lo, hi = flt.window(n, start, end)
+    count = end - start
+    y_ref, pk_ref = None, None
+    for xs_pad, ys_pad in ((0, 0), (13, 7)):
+        xs, ys = (hi - lo) + xs_pad, count + ys_pad
+        xp = np.zeros((nch, xs), np.float32)
+        xp[:, :hi - lo] = x[:, lo:hi]
+        xp[:, hi - lo:] = 1e30  # never read
+        dx = lc.DeviceBuffer.from_array(xp)
+        dy = lc.DeviceBuffer.from_array(np.full((nch, ys), -7.0, np.float32))
+        dpk = lc.DeviceBuffer(4 * nch)
+        lc.peak_reset_dev(dpk, nch)
+        flt.filter_window_dev(dx, lo, hi, xs, n, nch, dy, start, ys, start, end, dpk)
+        lc.sync()
+        y = dy.download((nch, ys))
+        pk = dpk.download(nch)
+        for b in (dx, dy, dpk):
+            b.free()
+        assert np.all(y[:, count:] == -7.0)
+        if y_ref is None:
+            y_ref, pk_ref = y[:, :count].copy(), pk
+        else:
+            assert np.array_equal(y[:, :count], y_ref) and np.array_equal(pk, pk_ref)
+    ref, _ = oracle_mod.filter_points(x[1], taps, np.arange(start, end), oracle_mod.MODE_LD)
+    assert max_ulps(y_ref[1], ref) <= 1 and rms(y_ref[1], ref) <= RMS_TOL
