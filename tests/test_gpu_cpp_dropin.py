@@ -62,13 +62,16 @@ def dropin():
     return DROPIN
 
 
+@pytest.mark.parametrize("golden", ["random_int24", "impulse"])
 @pytest.mark.parametrize("threads", [1, 3, 8, 64])
-def test_reference_call_shape(dropin, tmp_path, oracle_mod, threads):
+def test_reference_call_shape(dropin, tmp_path, oracle_mod, threads, golden):
     """ProcessFile.cp:57-87 with apply_filter_range passed by name to std::thread
     (Diskerror::apply_filter_range of include/lcfir/FilterCore.h, reference
     parameter types), a WindowedSinc stand-in with only getMo2()/fms(): taps
-    recovered through fms, every chunk a concurrent lcfir_apply_range call."""
-    g = load_golden("random_int24")
+    recovered through fms, every chunk a concurrent lcfir_apply_range call.
+    random_int24 (401 taps) runs the FFT under AUTO, impulse (41 taps) the
+    direct kernel, which must also match the strict fma chain bit for bit."""
+    g = load_golden(golden)
     x, taps = g["x"], g["taps"]
     xi, ti, yo = tmp_path / "x.f32", tmp_path / "t.f64", tmp_path / "y.f32"
     np.ascontiguousarray(x, np.float32).tofile(xi)
@@ -86,6 +89,8 @@ def test_reference_call_shape(dropin, tmp_path, oracle_mod, threads):
         whole = np.zeros(x.shape[1], np.float32)
         flt.apply_range(np.ascontiguousarray(x[c], np.float32), whole, 0, x.shape[1])
         assert np.array_equal(y[c], whole), (threads, c)
+        if flt.method == "direct":
+            assert np.array_equal(y[c], oracle_mod.filter_channel(x[c], taps, oracle_mod.MODE_FMA)), c
         ref = oracle_mod.filter_channel(x[c], taps, oracle_mod.MODE_LD)
         d = y[c].astype(np.float64) - ref
         assert np.sqrt(np.mean(d * d)) <= 1e-9
