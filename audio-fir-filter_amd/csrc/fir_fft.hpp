@@ -197,14 +197,6 @@ inline int fft_partition_count(int ntaps, int L = 16384) {
     }
     return best;
 }
-// The launch a plan is chosen for (fft_choose_seg_len): outputs per channel
-// and channels of the first call that builds it, and the device's CUs.
-// outputs = 0: no call known (the per-output cost decides).
-struct FftShape {
-    int64_t outputs = 0;
-    int nch = 1;
-    int cus = 256;
-};
 // Time of one unit relative to a single-partition L = 16 384 unit, measured
 // on MI355X with tools/fft32_trace.hip (config-3 shape, 6 001 .. 30 001 taps,
 // DESIGN.md s4.2): a partitioned L = 16 384 pass also reads and writes its f64
@@ -215,32 +207,28 @@ inline double fft_unit_cost(int L, int parts, bool sym) {
     if (L == 16384) return parts == 1 ? 1.0 : 1.25;
     return parts == 1 ? (sym ? 2.9 : 3.1) : 4.0;
 }
-// Estimated time of a launch of `shape` with segment length L: partitions x
-// rounds of the persistent grid x unit cost (or, without a shape, the cost per
-// output).  Infinity when L cannot hold the filter.
-inline double fft_seg_estimate(const std::vector<double> &h, int L, const FftShape &shape, const FftTuning &tune);
-// Segment length for a filter (FftTuning::seg_len = 0): the lower estimate
-// for the first call's shape, the longer segment only when it saves at least
-// 5 %.  Per filter, not per call: the segment grid must not change under a
-// ctx (partition invariance, fft_grid_start).  Long launches of long filters
-// take L = 32 768 (one partition up to 30 721 taps instead of two from
-// 10 900, 2x faster at 12 001 .. 19 201 taps); short ones, where a 2.9x longer
-// unit is the whole launch, keep L = 16 384 (config 1: 48 000 samples).
-inline int fft_choose_seg_len(const std::vector<double> &h, const FftShape &shape, const FftTuning &tune) {
-    const double c16 = fft_seg_estimate(h, 16384, shape, tune), c32 = fft_seg_estimate(h, 32768, shape, tune);
-    return c32 < 0.95 * c16 ? 32768 : 16384;
-}
-
-inline double fft_seg_estimate(const std::vector<double> &h, int L, const FftShape &shape, const FftTuning &tune) {
+// Estimated time per output with segment length L: partitions x unit cost /
+// outputs per segment.  Infinity when L cannot hold the filter.
+inline double fft_seg_estimate(const std::vector<double> &h, int L, const FftTuning &tune) {
     const int ntaps = (int)h.size();
     const int parts = fft_partition_count(ntaps, L);
     if (parts == 0) return 1e300;
     const int B = L - (parts == 1 ? ntaps : fft_partition_taps(ntaps, parts)) + 1;
-    const double unit = fft_unit_cost(L, parts, fft_sym_eligible(h, parts, tune));
-    if (shape.outputs <= 0) return unit * parts / (double)B;
-    const int64_t units = (int64_t)std::max(shape.nch, 1) * ((shape.outputs + B - 1) / B);
-    const int cus = std::max(shape.cus, 1);
-    return unit * parts * (double)((units + cus - 1) / cus);
+    return fft_unit_cost(L, parts, fft_sym_eligible(h, parts, tune)) * parts / (double)B;
+}
+// Segment length for a filter (FftTuning::seg_len = 0): the lower cost per
+// output, the longer segment only when it saves at least 5 %.  A function of
+// the taps and the tuning alone, never of a call's shape: the segment grid
+// must not change under a ctx (partition invariance, fft_grid_start), and
+// every entry point (range, window, channels, fft_info), every --devices
+// stage and every rank then builds the same plan for the same filter, so a
+// file's bytes do not depend on which call came first.  Long
+// filters take L = 32 768 (one partition up to 30 721 taps instead of two
+// from 10 900, 2x faster at 12 001 .. 19 201 taps); config 1's 48 000-sample
+// launch at 19 201 taps measured equal either way (0.0386 vs 0.0387 ms, the
+// graph-replayed step 3 % faster with 32 768).
+inline int fft_choose_seg_len(const std::vector<double> &h, const FftTuning &tune) {
+    return fft_seg_estimate(h, 32768, tune) < 0.95 * fft_seg_estimate(h, 16384, tune) ? 32768 : 16384;
 }
 
 // LDS slot of column c: a wave's two columns sit in adjacent 8 KiB blocks
@@ -1273,12 +1261,11 @@ struct FftTables {
     std::vector<double2> tw;   // kFftTw or kFft32Tw
 };
 
-inline FftTables fft_plan_tables(const std::vector<double> &taps, const FftTuning &tune,
-                                 const FftShape &shape = FftShape{}) {
+inline FftTables fft_plan_tables(const std::vector<double> &taps, const FftTuning &tune) {
     const int ntaps = (int)taps.size();
-    // segment length: the tuning's, else the estimate's for the first call's
-    // shape; L = 32768 runs fir_fft32.hpp's two 8192-point halves (bins of each parity)
-    const int L = tune.seg_len ? tune.seg_len : fft_choose_seg_len(taps, shape, tune);
+    // segment length: the tuning's, else the filter's cheaper one per output;
+    // L = 32768 runs fir_fft32.hpp's two 8192-point halves (bins of each parity)
+    const int L = tune.seg_len ? tune.seg_len : fft_choose_seg_len(taps, tune);
     const int halves = L == kFft32L ? 2 : 1;
     const int Mf = L / 2; // complex transform length
     const int parts = fft_partition_count(ntaps, L);
@@ -1383,7 +1370,7 @@ inline FftTables fft_plan_tables(const std::vector<double> &taps, const FftTunin
 }
 
 inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, const FftTuning &tune, hipStream_t s,
-                           std::string &err, FftShape shape = FftShape{}) {
+                           std::string &err) {
     if (!fft_supported(ntaps)) {
         err = "tap count outside the FFT method's range";
         return false;
@@ -1400,8 +1387,7 @@ inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, const
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
         cus > 0)
         plan.cus = cus;
-    shape.cus = plan.cus;
-    const FftTables T = fft_plan_tables(taps, tune, shape);
+    const FftTables T = fft_plan_tables(taps, tune);
     const std::vector<double2> &pair = T.pair, &tw = T.tw;
     const std::vector<uint32_t> &task = T.task;
     // stream-ordered on the ctx's own stream s (freed the same way, fft_plan_free)

@@ -18,6 +18,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -58,6 +59,11 @@ struct lcfir_ctx {
     };
     std::vector<Scratch> scratch;
     std::vector<double *> retired; // outgrown scratch that a captured graph may still use
+    // a HIP graph captured a launch of the current plan: its tables (kernel
+    // arguments of that graph) are retired, not freed, when the tuning drops
+    // the plan (lcfir_ctx_set_fft_tuning), and freed by lcfir_ctx_destroy
+    bool plan_captured = false;
+    std::vector<lcfir::FftPlan> retired_plans;
 };
 
 namespace {
@@ -141,20 +147,16 @@ int resolve_method(lcfir_ctx *ctx) {
     return lcfir::fft_preferred(ctx->ntaps) ? LCFIR_METHOD_FFT : LCFIR_METHOD_DIRECT;
 }
 
-// The FFT plan, built at the first use: its segment length (unless tuned) is
-// chosen for that call's shape, the channel length x nch (0: unknown),
-// lcfir::fft_choose_seg_len.  The channel's length, not the call's range:
-// every range of a channel -- the reference's per-thread chunks, the ranks of
-// a split file -- then gets the same plan, hence the same segment grid and
-// the same bytes, whichever call comes first.
-int ensure_fft(lcfir_ctx *ctx, int64_t outputs = 0, int nch = 1) {
+// The FFT plan, built at the first use.  Its segment length (unless tuned) is
+// a function of the taps alone (lcfir::fft_choose_seg_len), so every call on
+// a ctx -- the reference's per-thread ranges, a rank's window of a split
+// file, a multi-channel launch, fft_info -- runs the same segment grid and
+// gives the same bytes, whichever comes first.
+int ensure_fft(lcfir_ctx *ctx) {
     std::lock_guard<std::mutex> lk(ctx->fft_mu);
     if (ctx->fft.ready) return LCFIR_OK;
     std::string err;
-    lcfir::FftShape shape;
-    shape.outputs = outputs;
-    shape.nch = nch;
-    if (!lcfir::fft_plan_build(ctx->fft, ctx->d_taps, ctx->ntaps, ctx->tune, ctx->own, err, shape))
+    if (!lcfir::fft_plan_build(ctx->fft, ctx->d_taps, ctx->ntaps, ctx->tune, ctx->own, err))
         return fail(LCFIR_EDEVICE, "fft plan: %s", err.c_str());
     return LCFIR_OK;
 }
@@ -216,7 +218,7 @@ int launch_normalize(float *d_y, int64_t stride, int32_t nch, int64_t n, const u
 // track_stream: remember s for lcfir_ctx_destroy's wait (false for the
 // staging streams of lcfir_apply_range, which synchronises its stream before
 // returning and may destroy it later, lcfir_staging_release).
-int run_filter(lcfir_ctx *ctx, lcfir::DirectParams p, int nch, hipStream_t s, int64_t chan_n,
+int run_filter(lcfir_ctx *ctx, lcfir::DirectParams p, int nch, hipStream_t s,
                const lcfir::FftNrm *nrm = nullptr, bool track_stream = true) {
     p.taps = ctx->d_taps;
     p.ntaps = ctx->ntaps;
@@ -224,8 +226,13 @@ int run_filter(lcfir_ctx *ctx, lcfir::DirectParams p, int nch, hipStream_t s, in
     if (track_stream) note_stream(ctx, s);
     const int m = resolve_method(ctx);
     if (m == LCFIR_METHOD_FFT) {
-        int rc = ensure_fft(ctx, chan_n, nch);
+        int rc = ensure_fft(ctx);
         if (rc) return rc;
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive) {
+            std::lock_guard<std::mutex> lk(ctx->fft_mu);
+            ctx->plan_captured = true;
+        }
         std::string err;
         // per-stream scratch: the L = 32768 kernel's park slabs, then the
         // partitioned filters' f64 partial sums
@@ -258,6 +265,15 @@ bool ranges_overlap(const void *a, size_t an, const void *b, size_t bn) {
 }
 
 // ---- staging pool for the host-pointer entry point ------------------------
+// The reference's buffers are pageable (std::vector inside VectorMath).  A
+// slot moves them through two pinned bounce buffers of its own, chunk by
+// chunk: the host thread copies chunk i into one while the DMA engine moves
+// chunk i-1 out of the other (LCFIR_STAGING_BOUNCE, the default), instead of
+// handing the pageable pointer to hipMemcpyAsync (LCFIR_STAGING_PAGEABLE, the
+// round-3 behaviour).  Caller memory that is already pinned (hipHostMalloc,
+// hipHostRegister) is copied directly in either mode.
+constexpr size_t kBounceBytes = (size_t)4 << 20;
+
 struct Staging {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -265,7 +281,106 @@ struct Staging {
     size_t x_cap = 0;
     float *d_y = nullptr;
     size_t y_cap = 0;
+    void *h_bounce[2] = {nullptr, nullptr}; // pinned, kBounceBytes each (lazily)
+    hipEvent_t bev[2] = {nullptr, nullptr}; // the last DMA touching h_bounce[b] is done
+    hipEvent_t tev[4] = {};                 // lcfir_range_profile: H2D start/end, kernel end, D2H end
 };
+
+std::atomic<int> g_staging_mode{LCFIR_STAGING_BOUNCE};
+std::atomic<int> g_range_profile{0};
+std::mutex g_stats_mu;
+lcfir_range_stats g_stats{};
+
+// [p, p + bytes) lies in page-locked host memory the DMA engine can read
+bool host_pinned(const void *p, size_t bytes) {
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess || a.type != hipMemoryTypeHost) {
+        (void)hipGetLastError();
+        return false;
+    }
+    if (bytes > 1) {
+        hipPointerAttribute_t b{};
+        if (hipPointerGetAttributes(&b, static_cast<const char *>(p) + bytes - 1) != hipSuccess ||
+            b.type != hipMemoryTypeHost) {
+            (void)hipGetLastError();
+            return false;
+        }
+    }
+    return true;
+}
+
+int ensure_bounce(Staging *st) {
+    for (int b = 0; b < 2; ++b) {
+        if (!st->h_bounce[b] && hipHostMalloc(&st->h_bounce[b], kBounceBytes, hipHostMallocDefault) != hipSuccess) {
+            st->h_bounce[b] = nullptr;
+            return fail(LCFIR_ENOMEM, "hipHostMalloc(%zu) for a staging bounce buffer failed", kBounceBytes);
+        }
+        if (!st->bev[b] && hipEventCreateWithFlags(&st->bev[b], hipEventDisableTiming) != hipSuccess) {
+            st->bev[b] = nullptr;
+            return fail(LCFIR_EDEVICE, "event creation failed");
+        }
+    }
+    return LCFIR_OK;
+}
+
+// Host -> device on the slot's stream.  Pageable source in bounce mode: chunk
+// i is copied into bounce i mod 2 once the DMA of chunk i - 2 has left it.
+// Returns with the DMAs queued (the host copies done).
+int h2d_staged(Staging *st, void *dst, const void *src, size_t bytes, bool &staged) {
+    staged = false;
+    if (g_staging_mode.load(std::memory_order_relaxed) == LCFIR_STAGING_PAGEABLE || host_pinned(src, bytes)) {
+        LCFIR_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st->stream));
+        return LCFIR_OK;
+    }
+    if (const int rc = ensure_bounce(st)) return rc;
+    staged = true;
+    auto *d = static_cast<char *>(dst);
+    auto *s = static_cast<const char *>(src);
+    for (size_t off = 0, i = 0; off < bytes; off += kBounceBytes, ++i) {
+        const int b = (int)(i & 1);
+        const size_t len = std::min(kBounceBytes, bytes - off);
+        if (i >= 2) LCFIR_HIP(hipEventSynchronize(st->bev[b]));
+        std::memcpy(st->h_bounce[b], s + off, len);
+        LCFIR_HIP(hipMemcpyAsync(d + off, st->h_bounce[b], len, hipMemcpyHostToDevice, st->stream));
+        LCFIR_HIP(hipEventRecord(st->bev[b], st->stream));
+    }
+    return LCFIR_OK;
+}
+
+// Device -> host after the work queued on the slot's stream; returns once
+// dst holds the bytes (stream order: the DMAs wait for the kernel).  If
+// `tev_end` is set it is recorded after the last DMA.
+int d2h_staged(Staging *st, void *dst, const void *src, size_t bytes, hipEvent_t tev_end) {
+    if (g_staging_mode.load(std::memory_order_relaxed) == LCFIR_STAGING_PAGEABLE || host_pinned(dst, bytes)) {
+        LCFIR_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st->stream));
+        if (tev_end) LCFIR_HIP(hipEventRecord(tev_end, st->stream));
+        LCFIR_HIP(hipStreamSynchronize(st->stream));
+        return LCFIR_OK;
+    }
+    if (const int rc = ensure_bounce(st)) return rc;
+    auto *d = static_cast<char *>(dst);
+    auto *s = static_cast<const char *>(src);
+    const size_t n = (bytes + kBounceBytes - 1) / kBounceBytes;
+    auto enqueue = [&](size_t i) -> int {
+        const int b = (int)(i & 1);
+        const size_t off = i * kBounceBytes, len = std::min(kBounceBytes, bytes - off);
+        LCFIR_HIP(hipMemcpyAsync(st->h_bounce[b], s + off, len, hipMemcpyDeviceToHost, st->stream));
+        LCFIR_HIP(hipEventRecord(st->bev[b], st->stream));
+        if (tev_end && i + 1 == n) LCFIR_HIP(hipEventRecord(tev_end, st->stream));
+        return LCFIR_OK;
+    };
+    for (size_t i = 0; i < n && i < 2; ++i)
+        if (const int rc = enqueue(i)) return rc;
+    for (size_t i = 0; i < n; ++i) {
+        const int b = (int)(i & 1);
+        const size_t off = i * kBounceBytes, len = std::min(kBounceBytes, bytes - off);
+        LCFIR_HIP(hipEventSynchronize(st->bev[b]));
+        std::memcpy(d + off, st->h_bounce[b], len);
+        if (i + 2 < n)
+            if (const int rc = enqueue(i + 2)) return rc;
+    }
+    return LCFIR_OK;
+}
 
 // Slots per device: enough streams to keep a GPU busy from host threads (each
 // call is synchronous on its slot), few enough that the reference's default
@@ -284,6 +399,12 @@ void free_staging(Staging *s) {
     if (s->d_y) (void)hipFreeAsync(s->d_y, s->stream);
     (void)hipStreamSynchronize(s->stream);
     (void)hipStreamDestroy(s->stream);
+    for (int b = 0; b < 2; ++b) {
+        if (s->h_bounce[b]) (void)hipHostFree(s->h_bounce[b]);
+        if (s->bev[b]) (void)hipEventDestroy(s->bev[b]);
+    }
+    for (hipEvent_t e : s->tev)
+        if (e) (void)hipEventDestroy(e);
     delete s;
 }
 
@@ -420,6 +541,7 @@ int lcfir_ctx_destroy(lcfir_ctx *ctx) {
     for (auto &e : ctx->scratch)
         if (e.p) (void)hipFreeAsync(e.p, ctx->own);
     for (double *p : ctx->retired) (void)hipFreeAsync(p, ctx->own);
+    for (lcfir::FftPlan &rp : ctx->retired_plans) lcfir::fft_plan_free(rp, ctx->own);
     lcfir::fft_plan_free(ctx->fft, ctx->own);
     if (ctx->d_taps) (void)hipFreeAsync(ctx->d_taps, ctx->own);
     if (ctx->own) {
@@ -491,7 +613,14 @@ int lcfir_ctx_set_fft_tuning(lcfir_ctx *ctx, int32_t seg_len, int32_t zero_phase
         std::lock_guard<std::mutex> lk2(ctx->streams_mu);
         for (hipStream_t s : ctx->used) (void)hipStreamSynchronize(s);
     }
-    lcfir::fft_plan_free(ctx->fft, ctx->own);
+    if (ctx->plan_captured) {
+        // a captured graph still passes these tables to its kernels
+        ctx->retired_plans.push_back(ctx->fft);
+        ctx->fft = lcfir::FftPlan{};
+        ctx->plan_captured = false;
+    } else {
+        lcfir::fft_plan_free(ctx->fft, ctx->own);
+    }
     LCFIR_HIP(hipStreamSynchronize(ctx->own));
     ctx->tune.seg_len = seg_len;
     ctx->tune.zero_phase = zero_phase;
@@ -505,7 +634,7 @@ static int range_window(lcfir_ctx *ctx, int64_t n, int64_t start, int64_t end, i
     lo = start - ctx->half;
     hi = end + ctx->half;
     if (resolve_method(ctx) == LCFIR_METHOD_FFT) {
-        const int rc = ensure_fft(ctx, n, 1);
+        const int rc = ensure_fft(ctx);
         if (rc) return rc;
         lcfir::fft_window(ctx->fft, ctx->half, start, end, lo, hi);
     }
@@ -546,15 +675,25 @@ int lcfir_apply_range(lcfir_ctx *ctx, const float *x, int64_t n, float *y, int64
     // whole-channel outputs bit for bit (ProcessFile.cp:60-83 at any -t)
     int64_t lo = 0, hi = 0;
     if (const int wrc = range_window(ctx, n, start, end, lo, hi)) return wrc;
+    const auto t_call = std::chrono::steady_clock::now();
     Staging *st = borrow_staging(ctx->device);
     if (!st) return fail(LCFIR_EDEVICE, "stream creation failed");
+    const bool prof = g_range_profile.load(std::memory_order_relaxed) != 0;
     int rc = grow(st->d_x, st->x_cap, (size_t)(hi - lo), st->stream);
     if (!rc) rc = grow(st->d_y, st->y_cap, (size_t)(end - start), st->stream);
-    if (!rc) {
-        if (hipMemcpyAsync(st->d_x, x + lo, sizeof(float) * (size_t)(hi - lo),
-                           hipMemcpyHostToDevice, st->stream) != hipSuccess)
-            rc = fail(LCFIR_EDEVICE, "H2D copy failed");
-    }
+    if (!rc && prof)
+        for (hipEvent_t &e : st->tev)
+            if (!e && hipEventCreate(&e) != hipSuccess) {
+                e = nullptr;
+                rc = fail(LCFIR_EDEVICE, "event creation failed");
+                break;
+            }
+    if (!rc && prof && hipEventRecord(st->tev[0], st->stream) != hipSuccess)
+        rc = fail(LCFIR_EDEVICE, "event record failed");
+    bool staged = false;
+    if (!rc) rc = h2d_staged(st, st->d_x, x + lo, sizeof(float) * (size_t)(hi - lo), staged);
+    if (!rc && prof && hipEventRecord(st->tev[1], st->stream) != hipSuccess)
+        rc = fail(LCFIR_EDEVICE, "event record failed");
     if (!rc) {
         lcfir::DirectParams p{};
         p.x = st->d_x;
@@ -567,20 +706,59 @@ int lcfir_apply_range(lcfir_ctx *ctx, const float *x, int64_t n, float *y, int64
         p.start = start;
         p.end = end;
         p.peak = nullptr;
-        rc = run_filter(ctx, p, 1, st->stream, n, nullptr, /*track_stream=*/false);
+        rc = run_filter(ctx, p, 1, st->stream, nullptr, /*track_stream=*/false);
     }
-    if (!rc) {
-        if (hipMemcpyAsync(y + start, st->d_y, sizeof(float) * (size_t)(end - start),
-                           hipMemcpyDeviceToHost, st->stream) != hipSuccess)
-            rc = fail(LCFIR_EDEVICE, "D2H copy failed");
-    }
+    if (!rc && prof && hipEventRecord(st->tev[2], st->stream) != hipSuccess)
+        rc = fail(LCFIR_EDEVICE, "event record failed");
+    if (!rc) rc = d2h_staged(st, y + start, st->d_y, sizeof(float) * (size_t)(end - start), prof ? st->tev[3] : nullptr);
     if (!rc) {
         hipError_t e = hipStreamSynchronize(st->stream);
         if (e != hipSuccess) rc = fail(LCFIR_EDEVICE, "kernel failed: %s", hipGetErrorString(e));
     }
+    if (!rc) {
+        float ms[3] = {0, 0, 0};
+        if (prof)
+            for (int i = 0; i < 3; ++i) (void)hipEventElapsedTime(&ms[i], st->tev[i], st->tev[i + 1]);
+        const double wall =
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_call).count();
+        std::lock_guard<std::mutex> lk(g_stats_mu);
+        g_stats.calls += 1;
+        g_stats.samples += (uint64_t)(end - start);
+        g_stats.h2d_bytes += sizeof(float) * (uint64_t)(hi - lo);
+        g_stats.d2h_bytes += sizeof(float) * (uint64_t)(end - start);
+        g_stats.staged_calls += staged ? 1 : 0;
+        g_stats.wall_ms += wall;
+        if (prof) {
+            g_stats.profiled_calls += 1;
+            g_stats.h2d_ms += ms[0];
+            g_stats.kernel_ms += ms[1];
+            g_stats.d2h_ms += ms[2];
+        }
+    }
+    if (rc) (void)hipStreamSynchronize(st->stream); // no DMA of this call may still touch the bounce buffers
     return_staging(st);
     if (!rc && progress) progress(user, (uint64_t)(end - start));
     return rc;
+}
+
+int lcfir_staging_set_mode(int mode) {
+    if (mode != LCFIR_STAGING_BOUNCE && mode != LCFIR_STAGING_PAGEABLE)
+        return fail(LCFIR_EINVAL, "unknown staging mode %d", mode);
+    g_staging_mode.store(mode);
+    return LCFIR_OK;
+}
+
+int lcfir_range_profile(int enable) {
+    g_range_profile.store(enable ? 1 : 0);
+    return LCFIR_OK;
+}
+
+int lcfir_range_stats_get(lcfir_range_stats *out, int reset) {
+    if (!out) return fail(LCFIR_EINVAL, "out is null");
+    std::lock_guard<std::mutex> lk(g_stats_mu);
+    *out = g_stats;
+    if (reset) g_stats = lcfir_range_stats{};
+    return LCFIR_OK;
 }
 
 int lcfir_staging_release(int device) {
@@ -632,7 +810,7 @@ int lcfir_apply_range_dev(lcfir_ctx *ctx, const float *d_x, int64_t n, float *d_
     p.y_lo = 0;
     p.start = start;
     p.end = end;
-    return run_filter(ctx, p, 1, reinterpret_cast<hipStream_t>(stream), n);
+    return run_filter(ctx, p, 1, reinterpret_cast<hipStream_t>(stream));
 }
 
 int lcfir_filter_channels_dev(lcfir_ctx *ctx, const float *d_x, int64_t x_stride, int32_t nch,
@@ -660,7 +838,7 @@ int lcfir_filter_channels_dev(lcfir_ctx *ctx, const float *d_x, int64_t x_stride
     p.end = n;
     p.peak = d_peak ? peak_bits(d_peak) : nullptr;
     p.peak_stride = 1;
-    return run_filter(ctx, p, nch, reinterpret_cast<hipStream_t>(stream), n);
+    return run_filter(ctx, p, nch, reinterpret_cast<hipStream_t>(stream));
 }
 
 static int filter_window(lcfir_ctx *ctx, const float *d_xw, int64_t x_lo, int64_t x_hi, int64_t x_stride,
@@ -698,7 +876,7 @@ static int filter_window(lcfir_ctx *ctx, const float *d_xw, int64_t x_lo, int64_
     p.end = end;
     p.peak = d_peak ? peak_bits(d_peak) : nullptr;
     p.peak_stride = peak_stride;
-    return run_filter(ctx, p, nch, reinterpret_cast<hipStream_t>(stream), n, nrm);
+    return run_filter(ctx, p, nch, reinterpret_cast<hipStream_t>(stream), nrm);
 }
 
 int lcfir_filter_window_dev(lcfir_ctx *ctx, const float *d_xw, int64_t x_lo, int64_t x_hi,

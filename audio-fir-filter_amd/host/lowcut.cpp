@@ -396,29 +396,46 @@ struct GpuStage {
 void run_stage(GpuStage &st, Channel<Job> &to_writer, PinnedPool &pool, const Options &o) {
     FilterSet filters(o, st.device);
     Slot slots[2];
+    // the file being finished or enqueued when a step throws: the batch stops
+    // there (main.cp:131-146), so files of this stage with a lower index --
+    // at most the other slot's, enqueued earlier -- are still finished and
+    // handed to the writer
+    size_t at = (size_t)-1;
     try {
         for (auto &s : slots) check(lcfir_stream_create(st.device, &s.stream), "stream");
         size_t k = 0;
         while (auto j = st.in.pop()) {
             Slot &s = slots[k++ % 2];
             if (s.job) { // this slot's previous file is done once its stream drains
+                at = s.job->index;
                 finish_file(s, o);
                 to_writer.push(std::move(*s.job));
                 s.job.reset();
             }
             s.t0 = Clock::now();
             s.job.emplace(std::move(*j));
+            at = s.job->index;
             enqueue_file(s, *s.job, filters, pool, o);
         }
         for (size_t i = 0; i < 2; ++i) {
             Slot &s = slots[k++ % 2];
             if (!s.job) continue;
+            at = s.job->index;
             finish_file(s, o);
             to_writer.push(std::move(*s.job));
             s.job.reset();
         }
     } catch (...) {
         st.error = std::current_exception();
+        for (auto &s : slots) {
+            if (!s.job || s.job->index >= at) continue;
+            try {
+                finish_file(s, o);
+                to_writer.push(std::move(*s.job));
+            } catch (...) { // its stream failed too: the batch stops at the earlier file
+            }
+            s.job.reset();
+        }
         while (st.in.pop()) { // keep the reader from blocking on this stage
         }
     }

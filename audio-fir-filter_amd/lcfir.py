@@ -40,6 +40,19 @@ class LcfirError(RuntimeError):
 
 PROGRESS_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64)
 
+STAGING_BOUNCE, STAGING_PAGEABLE = 0, 1
+
+
+class RangeStats(ctypes.Structure):
+    """lcfir_range_stats (include/lcfir.h): accounting of lcfir_apply_range."""
+    _fields_ = [("calls", ctypes.c_uint64), ("samples", ctypes.c_uint64), ("h2d_bytes", ctypes.c_uint64),
+                ("d2h_bytes", ctypes.c_uint64), ("staged_calls", ctypes.c_uint64),
+                ("profiled_calls", ctypes.c_uint64), ("wall_ms", ctypes.c_double), ("h2d_ms", ctypes.c_double),
+                ("kernel_ms", ctypes.c_double), ("d2h_ms", ctypes.c_double)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
 _c_int, _c_i32, _c_i64 = ctypes.c_int, ctypes.c_int32, ctypes.c_int64
 _vp, _fp, _dp = ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_double)
 _ctxp = ctypes.c_void_p
@@ -61,6 +74,9 @@ _SIGNATURES = {
     "lcfir_apply_range": ([_ctxp, _vp, _c_i64, _vp, _c_i64, _c_i64, PROGRESS_FN, _vp], _c_int),
     "lcfir_staging_release": ([_c_int], _c_int),
     "lcfir_staging_count": ([_c_int, ctypes.POINTER(_c_int), ctypes.POINTER(_c_int)], _c_int),
+    "lcfir_staging_set_mode": ([_c_int], _c_int),
+    "lcfir_range_profile": ([_c_int], _c_int),
+    "lcfir_range_stats_get": ([_vp, _c_int], _c_int),
     "lcfir_apply_range_dev": ([_ctxp, _vp, _c_i64, _vp, _c_i64, _c_i64, _vp], _c_int),
     "lcfir_filter_channels_dev": (
         [_ctxp, _vp, _c_i64, _c_i32, _c_i64, _vp, _c_i64, _vp, _vp], _c_int),
@@ -348,6 +364,21 @@ def filter_channel(channel: np.ndarray, sinc: Filter, num_threads: int,
 def staging_release(device: int = -1):
     """Free the idle staging slots of lcfir_apply_range (-1: every device)."""
     _check(load().lcfir_staging_release(device))
+
+
+def staging_set_mode(mode: str):
+    """lcfir_staging_set_mode: 'bounce' (pinned chunks, default) or 'pageable'."""
+    _check(load().lcfir_staging_set_mode({"bounce": STAGING_BOUNCE, "pageable": STAGING_PAGEABLE}[mode]))
+
+
+def range_profile(enable: bool):
+    _check(load().lcfir_range_profile(1 if enable else 0))
+
+
+def range_stats(reset: bool = False) -> dict:
+    st = RangeStats()
+    _check(load().lcfir_range_stats_get(ctypes.byref(st), 1 if reset else 0))
+    return st.as_dict()
 
 
 def staging_count(device: int = 0):

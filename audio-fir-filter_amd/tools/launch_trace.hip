@@ -57,7 +57,11 @@ int main(int argc, char **argv) {
     CK(hipMemcpy(dt, taps.data(), sizeof(double) * T, hipMemcpyHostToDevice));
     lcfir::FftPlan plan;
     std::string err;
-    if (!lcfir::fft_plan_build(plan, dt, T, nullptr, err)) {
+    // the traced kernel is fir_fft_f64_kernel (L = 16 384); the L = 32 768 one
+    // has no unit stamps and would also need DirectParams::park
+    lcfir::FftTuning tune;
+    tune.seg_len = lcfir::kFftL;
+    if (!lcfir::fft_plan_build(plan, dt, T, tune, nullptr, err)) {
         std::fprintf(stderr, "plan: %s\n", err.c_str());
         return 1;
     }

@@ -118,6 +118,42 @@ def parse():
     return a
 
 
+def launch_plan(gpus, env):
+    """How this invocation runs `--gpus` ranks (one process per GPU):
+    'rank' -- it IS a rank: WORLD_SIZE is set (torch.distributed.run, the
+    driver's N > 1 launch) and equals --gpus, or neither is set and --gpus is 1;
+    'spawn' -- --gpus N > 1 without WORLD_SIZE: start N rank processes with
+    torch.distributed.run and wait for them (the parent never touches the GPU).
+    A WORLD_SIZE that disagrees with --gpus is an error, never a silent
+    single-GPU number recorded as the N-GPU point."""
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1, got {gpus}")
+    world = env.get("WORLD_SIZE")
+    if world is not None:
+        if int(world) != gpus:
+            raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {gpus}: launch {gpus} ranks "
+                             f"(torch.distributed.run --nproc-per-node {gpus}) or drop WORLD_SIZE")
+        return "rank"
+    return "rank" if gpus == 1 else "spawn"
+
+
+def spawn_ranks(gpus, argv):
+    """Run this script as `gpus` ranks under torch.distributed.run on 127.0.0.1
+    (a free port), as a CHILD process; returns its exit code.  Called before
+    anything initialises the GPU in this process (no exec: the children get
+    fresh processes)."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def design_taps(ntaps, fs):
     """Low-cut taps (dspguide Blackman windowed-sinc + spectral inversion),
     computed here in numpy so the product path never touches the oracle."""
@@ -144,6 +180,40 @@ def host_cores():
         return os.cpu_count() or 1
 
 
+def cgroup_cpu_quota(root="/sys/fs/cgroup"):
+    """The CPU bandwidth limit of this process's cgroup, in CPUs (quota /
+    period, rounded up), or None when unlimited or unreadable.  cgroup v2
+    `cpu.max` ("<quota> <period>" or "max <period>"), else v1
+    `cpu.cfs_quota_us` / `cpu.cfs_period_us`."""
+    import math
+    try:
+        with open(os.path.join(root, "cpu.max")) as f:
+            q, p = f.read().split()[:2]
+        if q == "max":
+            return None
+        return max(1, math.ceil(int(q) / int(p)))
+    except (OSError, ValueError):
+        pass
+    try:
+        with open(os.path.join(root, "cpu", "cpu.cfs_quota_us")) as f:
+            q = int(f.read().strip())
+        with open(os.path.join(root, "cpu", "cpu.cfs_period_us")) as f:
+            p = int(f.read().strip())
+        return None if q <= 0 or p <= 0 else max(1, math.ceil(q / p))
+    except (OSError, ValueError):
+        return None
+
+
+def usable_cpus(root="/sys/fs/cgroup"):
+    """(usable, affinity, quota): the CPUs this process can really keep busy
+    = min(affinity mask, cgroup quota).  On the GPU box the affinity mask
+    lists 256 CPUs while the job's share is 16, and 256 threads there run
+    slower than 16 (What's weak 5)."""
+    aff = host_cores()
+    quota = cgroup_cpu_quota(root)
+    return (min(aff, quota) if quota else aff), aff, quota
+
+
 def cpu_rate(oracle, x0, taps, threads, budget_s):
     """Msamples/s of the oracle's threaded restatement on a bounded prefix of
     x0 sized (by a short calibration run) to take about budget_s."""
@@ -161,15 +231,19 @@ def cpu_rate(oracle, x0, taps, threads, budget_s):
 def cpu_baseline(x0, taps, budget_s, single_thread=False):
     """Oracle restatement of the reference threaded CPU path (FilterCore.h +
     ProcessFile.cp:57-87, strict-order double FMA), on a bounded prefix, with
-    one thread per host core (nproc); beside it the reference's own default
-    thread count, floor(0.7 x hardware_concurrency) (main.cp:75-76)."""
+    one thread per usable CPU (min of the affinity mask and the cgroup CPU
+    quota); beside it the reference's own default thread count,
+    floor(0.7 x hardware_concurrency) (main.cp:75-76), hardware_concurrency
+    being the affinity count the reference would see."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    nproc = host_cores()
-    cores = 1 if single_thread else nproc
+    usable, nproc, quota = usable_cpus()
+    cores = 1 if single_thread else usable
     value, n, dt = cpu_rate(oracle, x0, taps, cores, budget_s)
     out = {"value": round(value, 4), "unit": "Msamples/s", "cores": cores, "kind": "port",
-           "nproc": nproc,
+           "nproc": nproc, "cgroup_cpu_quota": quota,
+           "cores_note": "cores = threads used = min(affinity mask, cgroup CPU quota) "
+                         "(1 for config 1, single-threaded as BASELINE.json states)",
            "sample": f"first {n} samples of file 0 (channels laid end to end), {taps.size} "
                      f"taps, oracle ORACLE_FMA three-loop restatement, {cores} pthreads, "
                      f"{dt:.1f} s"}
@@ -309,6 +383,8 @@ def preroll(step, seconds, sync, agree=None, batch=8):
 
 def main():
     args = parse()
+    if launch_plan(args.gpus, os.environ) == "spawn":
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -319,6 +395,9 @@ def main():
     if os.environ.get("LCFIR_BENCH_SHARE_DEVICE") == "1":
         # rehearsal of the multi-rank path on a box with fewer GPUs than ranks
         local %= max(1, torch.cuda.device_count())
+    elif local >= torch.cuda.device_count():
+        raise SystemExit(f"bench.py: rank {rank} needs GPU {local}, {torch.cuda.device_count()} visible "
+                         f"(--gpus {args.gpus}; LCFIR_BENCH_SHARE_DEVICE=1 rehearses ranks on fewer GPUs)")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:

@@ -83,14 +83,13 @@ int lcfir_ctx_ntaps(const lcfir_ctx *ctx, int32_t *ntaps);
  * count is outside the FFT method's range. */
 int lcfir_ctx_fft_info(lcfir_ctx *ctx, int32_t *seg_len, int32_t *parts, int32_t *zero_phase);
 /* Explicit FFT-method choices for this ctx (the library reads no environment
- * variables).  seg_len: 0 = automatic, or 16384 / 32768.  Automatic picks,
- * once per ctx when its plan is built (the first filter or window call), the
- * length with the lower estimated time for that call's channel length n and
- * channel count: tap partitions x persistent-grid rounds x the measured unit
- * cost (a 32768-sample unit costs 2.9 16384-sample ones).  The channel's
- * length, not the call's range, so every range of a channel (threads, ranks
- * of a split file) gets the same plan; window calls assume one channel,
- * fft_info (no length) the per-output cost.  zero_phase: 1 = linear-phase filters run in zero-phase form (the
+ * variables).  seg_len: 0 = automatic, or 16384 / 32768.  Automatic picks the
+ * length with the lower estimated time per output for the taps alone: tap
+ * partitions x the measured unit cost (a 32768-sample unit costs 2.9
+ * 16384-sample ones) / outputs per segment.  It never depends on a call's
+ * shape, so every call on a ctx (range, window, channels, fft_info; every
+ * thread, rank or device stage) runs the same plan and the same bytes,
+ * whichever call comes first.  zero_phase: 1 = linear-phase filters run in zero-phase form (the
  * default), 0 = always the general pair table; chunk: outputs per launch
  * chunk (0 = 2^28, else >= 4096); max_units: segments x channels per launch
  * (0 = 2^31 - 1).  Every setting gives outputs within 1 f32 ulp of every
@@ -129,6 +128,38 @@ int lcfir_apply_range(lcfir_ctx *ctx, const float *x, int64_t n, float *y, int64
  * lcfir_staging_count reports the slots in existence and the idle ones. */
 int lcfir_staging_release(int device);
 int lcfir_staging_count(int device, int *live, int *idle);
+/* How lcfir_apply_range moves the caller's (pageable) buffers over PCIe.
+ * BOUNCE (default): each staging slot owns two 4 MiB pinned buffers; the
+ * calling thread copies chunk i into one while the DMA engine moves chunk
+ * i - 1 out of the other, both ways.  PAGEABLE: the caller's pointers go to
+ * hipMemcpyAsync as they are (the runtime stages them itself).  Memory that
+ * is already pinned (hipHostMalloc / hipHostRegister) is copied directly in
+ * both modes.  Process-wide; takes effect at the next call. */
+typedef enum lcfir_staging_mode {
+    LCFIR_STAGING_BOUNCE = 0,
+    LCFIR_STAGING_PAGEABLE = 1
+} lcfir_staging_mode;
+int lcfir_staging_set_mode(int mode);
+/* Accounting of lcfir_apply_range calls since the last reset (process-wide).
+ * Always: calls, outputs, bytes each way, bounce-staged calls, the calls'
+ * host wall time (summed over calls, so concurrent calls add up).  With
+ * lcfir_range_profile(1) each call also records HIP events on its slot's
+ * stream (a few microseconds per call): H2D span (first host chunk copy to
+ * last DMA), kernel, D2H DMA span, summed over the profiled calls. */
+typedef struct lcfir_range_stats {
+    uint64_t calls;
+    uint64_t samples;
+    uint64_t h2d_bytes;
+    uint64_t d2h_bytes;
+    uint64_t staged_calls;
+    uint64_t profiled_calls;
+    double wall_ms;
+    double h2d_ms;
+    double kernel_ms;
+    double d2h_ms;
+} lcfir_range_stats;
+int lcfir_range_profile(int enable);
+int lcfir_range_stats_get(lcfir_range_stats *out, int reset);
 
 /* ---- device-resident variants (async on a hipStream_t passed as void*) -- */
 /* Same as lcfir_apply_range with device pointers; no host synchronisation. */

@@ -258,6 +258,42 @@ inline int &default_device() {
     return d;
 }
 
+namespace detail {
+// The filter of a sinc whose taps are reachable through data() / size(),
+// validated once per (sinc object, tap pointer, count, device) instead of on
+// every call: the reference calls apply_filter_range once per thread and
+// channel (ProcessFile.cp:71-78), and a fingerprint fms() plus a long-double
+// dot product over all T taps per call is host work growing with T (ADVICE
+// r03).  A hit costs one memcmp of the taps against the validated copy, so a
+// WindowedSinc rebuilt at the same address with other taps (the next file's)
+// misses.  nullptr when data() / size() are not consistent with getMo2() /
+// fms() (the caller then probes through fms()).
+template <class Channel, class Sinc>
+std::shared_ptr<Filter> direct_filter(const Sinc &sinc, const double *h, size_t T, int device) {
+    struct Entry {
+        const double *h;
+        size_t T;
+        int device;
+        std::vector<double> taps;
+        std::shared_ptr<Filter> flt;
+    };
+    static std::mutex mu;
+    static std::map<const void *, Entry> *cache = new std::map<const void *, Entry>; // never destroyed
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = cache->find(&sinc);
+        if (it != cache->end() && it->second.h == h && it->second.T == T && it->second.device == device &&
+            std::memcmp(it->second.taps.data(), h, T * sizeof(double)) == 0)
+            return it->second.flt;
+    }
+    if (!direct_taps_valid<Channel>(sinc, h, T)) return nullptr;
+    auto flt = FilterCache::instance().get(h, T, device);
+    std::lock_guard<std::mutex> lk(mu);
+    (*cache)[&sinc] = Entry{h, T, device, std::vector<double>(h, h + T), flt};
+    return flt;
+}
+} // namespace detail
+
 inline std::string &last_failure() {
     static thread_local std::string s;
     return s;
@@ -291,12 +327,9 @@ inline void apply_filter_range(const Channel &channel, const Sinc &sinc, Channel
                                int_fast64_t startIdx, int_fast64_t endIdx, Progress *progress) {
     try {
         std::shared_ptr<Filter> flt;
-        if constexpr (sinc_traits_direct<Sinc>::value) {
-            const double *h = SincTraits<Sinc>::data(sinc);
-            const size_t T = SincTraits<Sinc>::size(sinc);
-            if (detail::direct_taps_valid<Channel>(sinc, h, T))
-                flt = FilterCache::instance().get(h, T, default_device());
-        }
+        if constexpr (sinc_traits_direct<Sinc>::value)
+            flt = detail::direct_filter<Channel>(sinc, SincTraits<Sinc>::data(sinc), SincTraits<Sinc>::size(sinc),
+                                                 default_device());
         if (!flt) {
             if constexpr (sinc_has_fms<Channel, Sinc>::value) {
                 const auto taps = detail::probe_taps<Channel>(sinc);

@@ -3,10 +3,8 @@
 // apply_filter_range passed BY NAME to std::thread (ProcessFile.cp:71-78).
 //
 // VectorMath, WindowedSinc and ThreadSafeProgress come from the un-vendored
-// c_lib / ProgressBar.h; the stand-ins below expose only what FilterCore.h and
-// ProcessFile.cp use of them: VectorMath(size), size(), begin(), operator[],
-// max_mag(); WindowedSinc's getMo2() and fms(it[, count]) (no data()/size(), so
-// the drop-in must recover the taps through fms itself); report(size_t).
+// c_lib / ProgressBar.h; reference_types.hpp has stand-ins exposing only what
+// FilterCore.h and ProcessFile.cp use of them.
 //
 // usage: dropin_processfile in.f32 taps.f64 out.f32 nch n threads
 // Prints "progress <count>" and "peak <max|y|>".
@@ -20,65 +18,7 @@
 #include <thread>
 #include <vector>
 
-namespace Diskerror {
-
-template <class T>
-class VectorMath {
-public:
-    VectorMath() = default;
-    explicit VectorMath(size_t n) : v_(n) {}
-    size_t size() const { return v_.size(); }
-    typename std::vector<T>::const_iterator begin() const { return v_.begin(); }
-    typename std::vector<T>::iterator begin() { return v_.begin(); }
-    T &operator[](size_t i) { return v_[i]; }
-    const T &operator[](size_t i) const { return v_[i]; }
-    T max_mag() const {
-        T m = 0;
-        for (T x : v_) m = std::max(m, std::abs(x));
-        return m;
-    }
-
-private:
-    std::vector<T> v_;
-};
-
-// fms semantics as FilterCore.h calls it: fms(p) = all taps,
-// fms(p, -k) = the LAST k taps against p[0..k), fms(p, +k) = the FIRST k taps.
-template <class T>
-class WindowedSinc {
-public:
-    explicit WindowedSinc(std::vector<T> h) : h_(std::move(h)) {}
-    int getMo2() const { return (int)(h_.size() - 1) / 2; }
-    template <class It>
-    T fms(It p) const {
-        return fms(p, (int)h_.size());
-    }
-    template <class It>
-    T fms(It p, int count) const {
-        T acc = 0;
-        if (count >= 0) {
-            for (int k = 0; k < count; ++k) acc += h_[(size_t)k] * (T)p[k];
-        } else {
-            const size_t off = h_.size() - (size_t)(-count);
-            for (int k = 0; k < -count; ++k) acc += h_[off + (size_t)k] * (T)p[k];
-        }
-        return acc;
-    }
-
-private:
-    std::vector<T> h_;
-};
-
-class ThreadSafeProgress {
-public:
-    void report(size_t count) { counter_.fetch_add(count, std::memory_order_relaxed); }
-    size_t count() const { return counter_.load(); }
-
-private:
-    std::atomic<size_t> counter_{0};
-};
-
-} // namespace Diskerror
+#include "reference_types.hpp"
 
 #define LCFIR_DROPIN_TYPES_DECLARED
 #include "lcfir/FilterCore.h"

@@ -2,8 +2,8 @@
 // for a tap file, so a CPU test can emulate the kernels' pair step on them
 // (scripts/fft32_model.py).  No device is touched.
 //
-// usage: fft_tables_dump taps.f64 seg_len zero_phase out_prefix [outputs nch cus]
-// (the optional launch shape drives the segment-length choice at seg_len 0)
+// usage: fft_tables_dump taps.f64 seg_len zero_phase out_prefix
+// (seg_len 0: the library's own choice for the taps, fft_choose_seg_len)
 // writes <out_prefix>.meta (L halves parts tp sym, text), .pair .c8 .tw
 // (complex double pairs) and .task (uint32).
 #include <cstdio>
@@ -20,8 +20,8 @@ static void dump(const std::string &path, const std::vector<T> &v) {
 }
 
 int main(int argc, char **argv) {
-    if (argc != 5 && argc != 8) {
-        std::fprintf(stderr, "usage: %s taps.f64 seg_len zero_phase out_prefix [outputs nch cus]\n", argv[0]);
+    if (argc != 5) {
+        std::fprintf(stderr, "usage: %s taps.f64 seg_len zero_phase out_prefix\n", argv[0]);
         return 2;
     }
     std::ifstream f(argv[1], std::ios::binary | std::ios::ate);
@@ -33,13 +33,7 @@ int main(int argc, char **argv) {
     lcfir::FftTuning tune;
     tune.seg_len = std::atoi(argv[2]);
     tune.zero_phase = std::atoi(argv[3]);
-    lcfir::FftShape shape;
-    if (argc == 8) {
-        shape.outputs = std::atoll(argv[5]);
-        shape.nch = std::atoi(argv[6]);
-        shape.cus = std::atoi(argv[7]);
-    }
-    const lcfir::FftTables T = lcfir::fft_plan_tables(taps, tune, shape);
+    const lcfir::FftTables T = lcfir::fft_plan_tables(taps, tune);
     const std::string out = argv[4];
     std::ofstream m(out + ".meta");
     m << T.L << " " << T.halves << " " << T.parts << " " << T.tp << " " << (T.sym ? 1 : 0) << "\n";

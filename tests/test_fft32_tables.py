@@ -58,24 +58,19 @@ def test_tables_emulated_segment(dump, tmp_path, seg_len, ntaps, sym):
 
 
 def test_seg_len_choice(dump, tmp_path):
-    """fft_choose_seg_len (measured unit costs): without a
-    launch shape the per-output cost decides -- 16 384 up to config 3's 8 001
-    taps, 32 768 for 19 201 (one partition instead of two) and 38 401 (two
-    instead of five); with the first call's shape the persistent grid's rounds
-    decide -- config 1's 48 000 samples keep 16 384 at 19 201 taps (one round
-    either way, and an L = 32 768 unit costs 2.9), config 3's 8 x 5.76 M at
-    8 001 taps stays at 16 384, and long channels at 10 001 taps take 32 768."""
+    """fft_choose_seg_len (measured unit costs): a function of
+    the taps alone, the per-output cost decides -- 16 384 up to config 3's
+    8 001 taps, 32 768 from 10 001 (one unit 2.9x an L = 16 384 one for 3.6x
+    the outputs), for 19 201 (one partition instead of two; config 1's filter)
+    and 38 401 (two instead of five)."""
     import oracle
-    cases = [(401, None, 16384, 1), (4001, None, 16384, 1), (8001, None, 16384, 1), (19201, None, 32768, 1),
-             (38401, None, 32768, 2), (19201, (48000, 1), 16384, 2), (8001, (5_760_000, 8), 16384, 1),
-             (4001, (28_800_000, 2), 16384, 1), (10001, (5_760_000, 8), 32768, 1),
-             (19201, (172_800_000, 2), 32768, 1)]
-    for ntaps, shape, L, parts in cases:
+    cases = [(401, 16384, 1), (4001, 16384, 1), (8001, 16384, 1), (10001, 32768, 1), (12001, 32768, 1),
+             (19201, 32768, 1), (38401, 32768, 2)]
+    for ntaps, L, parts in cases:
         oracle.design_lowcut(20.0, 48000.0, ntaps).tofile(tmp_path / "t.f64")
-        extra = [str(shape[0]), str(shape[1]), "256"] if shape else []
-        subprocess.run([dump, str(tmp_path / "t.f64"), "0", "1", str(tmp_path / "tb")] + extra, check=True)
+        subprocess.run([dump, str(tmp_path / "t.f64"), "0", "1", str(tmp_path / "tb")], check=True)
         tb = fm.load_tables(str(tmp_path / "tb"))
-        assert (tb["L"], tb["parts"]) == (L, parts), (ntaps, shape)
+        assert (tb["L"], tb["parts"]) == (L, parts), ntaps
 
 
 def test_header_constants_match_model():

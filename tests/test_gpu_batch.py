@@ -594,3 +594,48 @@ def test_rccl_peak_exchange_world1(tt, oracle_mod, nccl_world1, lanes, normalize
         ref = files[f].copy()
         oracle_mod.process_buffer(ref, taps, nthreads=1, normalize=normalize, mode=oracle_mod.MODE_LD)
         assert _ulps(y, ref).max() <= 1, f
+
+
+@pytest.mark.parametrize("parts_taps", [4001, 19201])
+def test_graph_replay_after_fft_retuning(tt, oracle_mod, parts_taps):
+    """lcfir_ctx_set_fft_tuning drops the ctx's plan, but a HIP
+    graph captured earlier passes that plan's tables (pair table, twiddles,
+    task words) to its kernels: they are retired until lcfir_ctx_destroy, not
+    freed, so the graph still replays the captured bytes after a retune and
+    after eager calls that build and use the new plan.  19 201 taps at L =
+    16 384 forced: two partitions, so the per-stream scratch is captured too."""
+    torch, lc = tt
+    import synth
+    taps = oracle_mod.design_lowcut(20.0, 48000.0, parts_taps)
+    n = 120_000
+    x = synth.file_buffer(2, n, 48000.0, file=21, bits=24)
+    flt = lc.Filter(taps, method="fft")
+    flt.set_fft_tuning(seg_len=16384)
+    dx = torch.from_numpy(np.ascontiguousarray(x)).cuda()
+    dy = torch.zeros((2, n), dtype=torch.float32, device="cuda")
+    s = torch.cuda.Stream()
+    flt.filter_channels_dev(dx, n, 2, n, dy, n, None, stream=s.cuda_stream)  # eager: plan + scratch
+    torch.cuda.synchronize()
+    y0 = dy.cpu().numpy().copy()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        flt.filter_channels_dev(dx, n, 2, n, dy, n, None, stream=s.cuda_stream)
+    torch.cuda.synchronize()
+    flt.set_fft_tuning(seg_len=32768)  # the captured plan is dropped from the ctx
+    dy2 = torch.zeros((2, n), dtype=torch.float32, device="cuda")
+    flt.filter_channels_dev(dx, n, 2, n, dy2, n, None, stream=s.cuda_stream)  # the new plan
+    torch.cuda.synchronize()
+    assert flt.fft_info["seg_len"] == 32768
+    dy.zero_()
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s):
+        g.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(dy.cpu().numpy(), y0)
+    y2 = dy2.cpu().numpy()
+    for c in range(2):
+        idx = np.r_[np.arange(0, 50), np.arange(n - 50, n), np.arange(5000, n, 997)]
+        ref, _ = oracle_mod.filter_points(x[c], taps, idx, oracle_mod.MODE_LD)
+        assert rms(y2[c][idx], ref) <= RMS_TOL
+    del g
+    flt.close()

@@ -47,3 +47,25 @@ def test_bench_json_line(lanes):
     ing = d["ingest"]  # PCIe ingest probe: reported beside `value`, never in it
     assert ing["format"] == "s24le" and ing["decode_exact"] is True
     assert ing["bytes"] == 3 * ing["frames"] * ing["channels"] and 0 < ing["h2d_GBps"] < 200
+
+
+def test_bench_gpus2_spawns_two_ranks():
+    """`bench.py --gpus 2` started bare (no WORLD_SIZE) runs two ranks itself
+    (torch.distributed.run, one process per rank); on the one-GPU box they
+    share the device (LCFIR_BENCH_SHARE_DEVICE=1, gloo).  Config 5 with 2
+    files: one file per rank and the peak exchange of --normalize."""
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env["LCFIR_BENCH_SHARE_DEVICE"] = "1"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "5", "--files", "2",
+           "--seconds", "20", "--steps", "3", "--warmup", "1", "--preroll-s", "0.2", "--kernel-launches", "3",
+           "--no-ingest"]
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["files"] == 2
+    assert d["config"]["peak_exchange"] is True and d["config"]["normalize"] is True
+    assert d["parity"]["rms_vs_longdouble"] <= 1e-9
+    assert "cpu_baseline" not in d  # rank 0 at N = 1 only

@@ -95,3 +95,76 @@ def test_reference_call_shape(dropin, tmp_path, oracle_mod, threads, golden):
         d = y[c].astype(np.float64) - ref
         assert np.sqrt(np.mean(d * d)) <= 1e-9
         assert np.all(np.abs(d) <= np.spacing(np.abs(ref).astype(np.float32)).astype(np.float64))
+
+
+BENCH = os.path.join(ROOT, "tests", "cpp", "dropin_bench")
+
+
+def test_dropin_bench_short(dropin):
+    """tests/cpp/dropin_bench (the drop-in's timing tool, profiles/) on a 4-s
+    stereo file: both staging modes, 1 and 5 threads, every file bit-identical
+    to the one-launch device call, the stats and the per-call split filled."""
+    import json
+    r = subprocess.run([BENCH, "--seconds", "4", "--threads", "1,5", "--reps", "1"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr + r.stdout
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert [(d["mode"], d["threads"]) for d in lines] == [("bounce", 1), ("bounce", 5), ("pageable", 1),
+                                                          ("pageable", 5)]
+    for d in lines:
+        assert d["bit_identical"] is True and d["msamples_per_s"] > 0 and d["ntaps"] == 4001
+        assert d["calls_per_file"] == 2 * d["threads"]
+        assert d["staged_calls_frac"] == (1.0 if d["mode"] == "bounce" else 0.0)
+        sp = d["split_per_call_ms"]
+        assert sp["kernel"] > 0 and sp["h2d"] > 0 and sp["d2h"] > 0 and sp["wall"] > 0
+
+
+@pytest.mark.parametrize("mode", ["bounce", "pageable"])
+def test_apply_range_staging_modes(oracle_mod, mode):
+    """lcfir_apply_range through each staging mode and from pinned host
+    memory (copied directly): ranges that span several 4 MiB bounce chunks,
+    odd sizes and one-sample ranges, all equal to the device call's bytes."""
+    import lcfir
+    import synth
+    taps = oracle_mod.design_lowcut(20.0, 48000.0, 4001)
+    n = 3_000_001
+    x = np.ascontiguousarray(synth.file_buffer(1, n, 48000.0, file=31, bits=24)[0])
+    flt = lcfir.Filter(taps)
+    dx = lcfir.DeviceBuffer.from_array(x)
+    dy = lcfir.DeviceBuffer(4 * n)
+    flt.apply_range_dev(dx, n, dy, 0, n)
+    lcfir.sync()
+    want = dy.download(n)
+    lcfir.staging_set_mode(mode)
+    try:
+        lcfir.range_stats(reset=True)
+        y = np.full(n, 7.0, np.float32)
+        for start, end in [(0, 1_500_000), (1_500_000, 1_500_001), (1_500_001, n)]:
+            flt.apply_range(x, y, start, end)
+        assert np.array_equal(y, want)
+        st = lcfir.range_stats(reset=True)
+        assert st["calls"] == 3 and st["samples"] == n
+        assert st["staged_calls"] == (3 if mode == "bounce" else 0)
+        # pinned caller buffers: DMA straight from / to them
+        import ctypes
+        lib = lcfir.load()
+        px, py = ctypes.c_void_p(), ctypes.c_void_p()
+        assert lib.lcfir_host_malloc(4 * n, ctypes.byref(px)) == 0
+        assert lib.lcfir_host_malloc(4 * n, ctypes.byref(py)) == 0
+        try:
+            hx = np.ctypeslib.as_array((ctypes.c_float * n).from_address(px.value))
+            hy = np.ctypeslib.as_array((ctypes.c_float * n).from_address(py.value))
+            hx[:] = x
+            hy[:] = 7.0
+            flt.apply_range(hx, hy, 0, n)
+            assert np.array_equal(hy, want)
+            assert lcfir.range_stats(reset=True)["staged_calls"] == 0
+        finally:
+            lib.lcfir_host_free(px)
+            lib.lcfir_host_free(py)
+    finally:
+        lcfir.staging_set_mode("bounce")
+    idx = np.r_[np.arange(0, 20), np.arange(n - 20, n), np.arange(1000, n, 100_003)]
+    ref, _ = oracle_mod.filter_points(x, taps, idx, oracle_mod.MODE_LD)
+    d = want[idx].astype(np.float64) - ref
+    assert np.sqrt(np.mean(d * d)) <= 1e-9

@@ -187,6 +187,28 @@ def test_pipeline_stops_at_first_failure(tmp_path):
     assert not (outdir / "g2.wav").exists()
 
 
+def test_pipeline_gpu_stage_failure_keeps_earlier_files(tmp_path, oracle_mod):
+    """a failure inside the GPU stage (here the filter design for
+    file 2: -f 5000 is above its 8 kHz rate's Nyquist frequency) stops the
+    batch at that file, and the earlier file still in the stage's other slot
+    (file 1, enqueued before file 2) is finished and written.  Files 0 and 1
+    are written and correct, files 2 and 3 are not."""
+    specs = [48000, 48000, 8000, 48000]
+    srcs = []
+    for i, rate in enumerate(specs):
+        x = tone(1, 20000, rate)
+        p = tmp_path / f"s{i}.wav"
+        pcm_ref.write_wave(p, x, rate, "s24le")
+        srcs.append((p, pcm_ref.np_decode(pcm_ref.np_encode(x, "s24le"), "s24le", 1), rate))
+    outdir = tmp_path / "o"
+    args = ["-f", 5000, "-s", 2000, *[p for p, _, _ in srcs], outdir]
+    r = subprocess.run([LOWCUT, *map(str, args)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 1 and "design" in r.stderr, r.stderr + r.stdout
+    for p, xq, rate in srcs[:2]:
+        check_file(oracle_mod, p, outdir / p.name, xq, rate, "s24le", 5000, 2000, False)
+    assert not (outdir / "s2.wav").exists() and not (outdir / "s3.wav").exists()
+
+
 def test_large_file(tmp_path):
     """A 42 MB WAVE: every non-payload byte kept, and the payload equal to the
     same decode -> filter -> encode through the Python binding of the C ABI."""

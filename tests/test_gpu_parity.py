@@ -609,15 +609,15 @@ def test_fft_seg32_chunks_and_groups(lc, oracle_mod):
             assert max_ulps(ys[c], ref) <= 1 and rms(ys[c], ref) <= RMS_TOL, (n, c)
 
 
-@pytest.mark.parametrize("ntaps,n,nch,want_L", [(12001, 3_000_000, 2, 32768), (19201, 48_000, 1, 16384),
+@pytest.mark.parametrize("ntaps,n,nch,want_L", [(12001, 3_000_000, 2, 32768), (19201, 48_000, 1, 32768),
                                                 (8001, 600_000, 8, 16384)])
 def test_fft_auto_seg_len(lc, oracle_mod, ntaps, n, nch, want_L):
-    """The automatic segment length (fir_fft.hpp fft_choose_seg_len), chosen at
-    the first call from its shape: a long filter on long channels takes the
-    L = 32 768 segment (12 001 taps: one partition instead of two), config 1's
-    short channel keeps L = 16 384, and 8 001 taps (even costs) stays at
-    16 384.  The product path as it runs by default, against the long-double
-    oracle at every edge sample and random positions, fused peaks."""
+    """The automatic segment length (fir_fft.hpp fft_choose_seg_len), a
+    function of the taps: long filters take the L = 32 768 segment (12 001
+    taps: one partition instead of two; config 1's 19 201 taps on its short
+    channel too), and 8 001 taps (even costs) stays at 16 384.  The product
+    path as it runs by default, against the long-double oracle at every edge
+    sample and random positions, fused peaks."""
     import synth
     fs = 48000.0
     taps = oracle_mod.design_lowcut(20.0, fs, ntaps)
@@ -657,6 +657,28 @@ def test_fft_auto_seg_len_follows_the_channel(lc, oracle_mod):
     dy.free()
     assert whole.fft_info["seg_len"] == part.fft_info["seg_len"] == 32768
     assert np.array_equal(yr[start:end], y[0][start:end])
+
+
+@pytest.mark.parametrize("ntaps", [8001, 10001, 19201])
+def test_fft_plan_independent_of_first_call(lc, oracle_mod, ntaps):
+    """the plan (segment length, partitions) is a function of the
+    taps, so a ctx whose first call is lcfir_ctx_window (one channel assumed
+    before), one whose first call is a 2-channel filter_channels launch of a
+    short file and one asked fft_info first all run the same plan, and the
+    window-first ctx's bytes equal the channels-first ctx's."""
+    import synth
+    taps = oracle_mod.design_lowcut(20.0, 48000.0, ntaps)
+    n = 60_000  # short: the old shape model flipped 19 201 taps between lengths here
+    x = synth.file_buffer(2, n, 48000.0, file=15, bits=24)
+    chans = lc.Filter(taps, method="fft")
+    y_ch, _ = gpu_filter_channels(lc, chans, x)
+    win = lc.Filter(taps, method="fft")
+    lo, hi = win.window(n, 0, n)
+    info = lc.Filter(taps, method="fft")
+    assert win.fft_info == chans.fft_info == info.fft_info
+    y_win, _ = gpu_filter_channels(lc, win, x)
+    assert np.array_equal(y_ch, y_win)
+    assert (lo, hi) == (0, n)
 
 
 # ---- the loads' zero padding at every window alignment
