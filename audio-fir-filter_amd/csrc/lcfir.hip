@@ -265,13 +265,15 @@ bool ranges_overlap(const void *a, size_t an, const void *b, size_t bn) {
 }
 
 // ---- staging pool for the host-pointer entry point ------------------------
-// The reference's buffers are pageable (std::vector inside VectorMath).  A
-// slot moves them through two pinned bounce buffers of its own, chunk by
-// chunk: the host thread copies chunk i into one while the DMA engine moves
-// chunk i-1 out of the other (LCFIR_STAGING_BOUNCE, the default), instead of
-// handing the pageable pointer to hipMemcpyAsync (LCFIR_STAGING_PAGEABLE, the
-// round-3 behaviour).  Caller memory that is already pinned (hipHostMalloc,
-// hipHostRegister) is copied directly in either mode.
+// The reference's buffers are pageable (std::vector inside VectorMath).  By
+// default (LCFIR_STAGING_PAGEABLE) the caller's pointers go to hipMemcpyAsync
+// as they are: ROCm 7.2 moves large pageable ranges at 35 GB/s H2D and 29 GB/s
+// D2H from one thread, which a slot's own pinned bounce buffers
+// (LCFIR_STAGING_BOUNCE: the host thread copies chunk i into one while the
+// DMA engine moves chunk i - 1 out of the other) do not beat -- 24 / 24 GB/s
+// at one thread, and 4x slower H2D per call at 16 threads (tests/cpp/
+// dropin_bench, profiles/r04_dropin/).  Caller memory that is already pinned
+// (hipHostMalloc, hipHostRegister) is copied directly in either mode.
 constexpr size_t kBounceBytes = (size_t)4 << 20;
 
 struct Staging {
@@ -286,7 +288,7 @@ struct Staging {
     hipEvent_t tev[4] = {};                 // lcfir_range_profile: H2D start/end, kernel end, D2H end
 };
 
-std::atomic<int> g_staging_mode{LCFIR_STAGING_BOUNCE};
+std::atomic<int> g_staging_mode{LCFIR_STAGING_PAGEABLE};
 std::atomic<int> g_range_profile{0};
 std::mutex g_stats_mu;
 lcfir_range_stats g_stats{};

@@ -367,7 +367,8 @@ def staging_release(device: int = -1):
 
 
 def staging_set_mode(mode: str):
-    """lcfir_staging_set_mode: 'bounce' (pinned chunks, default) or 'pageable'."""
+    """lcfir_staging_set_mode: 'pageable' (default: the runtime stages the
+    caller's memory) or 'bounce' (the slot's pinned chunks)."""
     _check(load().lcfir_staging_set_mode({"bounce": STAGING_BOUNCE, "pageable": STAGING_PAGEABLE}[mode]))
 
 

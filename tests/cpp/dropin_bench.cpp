@@ -13,8 +13,10 @@
 // invariance); the tool exits 3 otherwise.  This is the host-pointer rate,
 // PCIe included: never bench.py's `value`.
 //
-// usage: dropin_bench [--seconds S] [--threads a,b,...] [--reps R] [--modes bounce,pageable]
+// usage: dropin_bench [--seconds S] [--threads a,b,...] [--reps R] [--modes pageable,bounce,pinned]
 //   --threads: counts; "ref" = floor(0.7 x hardware_concurrency) (main.cp:75-76)
+//   modes: the staging mode for pageable buffers, or "pinned": VectorMath's
+//   samples in page-locked memory (lcfir_host_malloc; copied directly)
 // Prints one JSON line per (mode, threads).
 #include <algorithm>
 #include <chrono>
@@ -53,13 +55,19 @@ static std::vector<std::string> split(const std::string &s) {
     return out;
 }
 
-// one file through ProcessFile.cp:57-87 (call shape unchanged); returns seconds
+// one file through ProcessFile.cp:57-87 (call shape unchanged); returns
+// seconds, and adds the span of temp_output's construction (ProcessFile.cp:58:
+// a zero-filled VectorMath of numFrames, page faults included) and of the
+// thread fan-out + join (:60-83, the drop-in calls) to *alloc_s / *fanout_s
 static double process_file(std::vector<VectorMath<float>> &buf, const WindowedSinc<double> &sinc,
-                           unsigned num_threads, ThreadSafeProgress &safe_progress) {
+                           unsigned num_threads, ThreadSafeProgress &safe_progress, double *alloc_s,
+                           double *fanout_s) {
     const auto t0 = Clock::now();
     for (size_t ch = 0; ch < buf.size(); ++ch) {
         const size_t numFrames = buf[ch].size();
+        const auto ta = Clock::now();
         VectorMath<float> temp_output(numFrames);
+        const auto tb = Clock::now();
         std::vector<std::thread> threads;
         threads.reserve(num_threads);
         const auto totalSamples = static_cast<int_fast64_t>(numFrames);
@@ -71,7 +79,10 @@ static double process_file(std::vector<VectorMath<float>> &buf, const WindowedSi
                                  start, end, &safe_progress);
         }
         for (auto &t : threads) t.join();
+        const auto tc = Clock::now();
         buf[ch] = std::move(temp_output);
+        *alloc_s += std::chrono::duration<double>(tb - ta).count();
+        *fanout_s += std::chrono::duration<double>(tc - tb).count();
     }
     return std::chrono::duration<double>(Clock::now() - t0).count();
 }
@@ -79,7 +90,7 @@ static double process_file(std::vector<VectorMath<float>> &buf, const WindowedSi
 int main(int argc, char **argv) {
     double seconds = 600.0;
     int reps = 3;
-    std::string threads_arg = "1,16,ref", modes_arg = "bounce,pageable";
+    std::string threads_arg = "1,16,ref", modes_arg = "pageable,bounce,pinned";
     for (int i = 1; i < argc; ++i) {
         const std::string a = argv[i];
         auto next = [&]() -> const char * {
@@ -94,7 +105,7 @@ int main(int argc, char **argv) {
         else if (a == "--reps") reps = std::max(1, std::atoi(next()));
         else if (a == "--modes") modes_arg = next();
         else {
-            std::fprintf(stderr, "usage: %s [--seconds S] [--threads a,b|ref] [--reps R] [--modes bounce,pageable]\n",
+            std::fprintf(stderr, "usage: %s [--seconds S] [--threads a,b|ref] [--reps R] [--modes pageable,bounce,pinned]\n",
                          argv[0]);
             return 2;
         }
@@ -140,10 +151,11 @@ int main(int argc, char **argv) {
     const unsigned ref_threads = std::max(1u, (unsigned)(0.7 * (double)hw)); // main.cp:75-76
     int bad = 0;
     for (const std::string &mode : split(modes_arg)) {
-        if (mode != "bounce" && mode != "pageable") {
+        if (mode != "bounce" && mode != "pageable" && mode != "pinned") {
             std::fprintf(stderr, "unknown mode %s\n", mode.c_str());
             return 2;
         }
+        vectormath_pinned() = mode == "pinned";
         if (lcfir_staging_set_mode(mode == "bounce" ? LCFIR_STAGING_BOUNCE : LCFIR_STAGING_PAGEABLE))
             die("mode");
         for (const std::string &t : split(threads_arg)) {
@@ -158,27 +170,29 @@ int main(int argc, char **argv) {
                 return buf;
             };
             ThreadSafeProgress progress;
+            double alloc_s = 0.0, fanout_s = 0.0;
             {
                 auto buf = fresh();
-                (void)process_file(buf, sinc, nt, progress); // warm-up: plan, slots, bounce buffers
+                (void)process_file(buf, sinc, nt, progress, &alloc_s, &fanout_s); // warm-up: plan, slots, bounce buffers
             }
+            alloc_s = fanout_s = 0.0;
             std::vector<double> times;
             bool identical = true;
             lcfir_range_stats st{};
             lcfir_range_stats_get(&st, 1);
             for (int r = 0; r < reps; ++r) {
                 auto buf = fresh();
-                times.push_back(process_file(buf, sinc, nt, progress));
+                times.push_back(process_file(buf, sinc, nt, progress, &alloc_s, &fanout_s));
                 for (size_t c = 0; c < nch; ++c)
                     identical = identical && std::memcmp(&buf[c][0], want.data() + c * n, sizeof(float) * n) == 0;
             }
             lcfir_range_stats_get(&st, 1);
             // one profiled file: the per-call stage split
             lcfir_range_profile(1);
-            double tprof;
+            double tprof, pa = 0.0, pf = 0.0;
             {
                 auto buf = fresh();
-                tprof = process_file(buf, sinc, nt, progress);
+                tprof = process_file(buf, sinc, nt, progress, &pa, &pf);
             }
             lcfir_range_profile(0);
             lcfir_range_stats sp{};
@@ -192,16 +206,21 @@ int main(int argc, char **argv) {
                 "{\"tool\": \"dropin_bench\", \"mode\": \"%s\", \"threads\": %u, \"hardware_concurrency\": %u, "
                 "\"channels\": %zu, \"samples_per_channel\": %zu, \"ntaps\": %d, \"reps\": %d, "
                 "\"msamples_per_s\": %.1f, \"msamples_per_s_best\": %.1f, \"ms_per_file\": %.3f, "
-                "\"h2d_bound_frac\": %.4f, \"bit_identical\": %s, \"calls_per_file\": %.0f, "
+                "\"h2d_bound_frac\": %.4f, \"fanout_msamples_per_s\": %.1f, \"fanout_h2d_bound_frac\": %.4f, "
+                "\"alloc_ms_per_file\": %.3f, \"fanout_ms_per_file\": %.3f, "
+                "\"bit_identical\": %s, \"calls_per_file\": %.0f, "
                 "\"staged_calls_frac\": %.3f, \"pcie_GBps_per_file\": %.2f, "
                 "\"split_per_call_ms\": {\"wall\": %.4f, \"h2d\": %.4f, \"kernel\": %.4f, \"d2h\": %.4f}, "
                 "\"split_sum_over_file_wall\": {\"h2d\": %.3f, \"kernel\": %.3f, \"d2h\": %.3f}, "
                 "\"profiled_file_ms\": %.3f, "
                 "\"note\": \"host-pointer drop-in (FilterCore.h through ProcessFile.cp:57-87's threads), "
-                "pageable buffers, PCIe both ways; h2d_bound_frac = rate / (56 GB/s pinned H2D / 4 B); "
-                "never bench.py value\"}\n",
+                "pageable buffers, PCIe both ways; msamples_per_s = the whole ProcessFile.cp:57-87 loop "
+                "(temp_output allocation included), fanout_* = the threads' spawn-to-join spans only (the "
+                "drop-in calls); h2d_bound_frac = rate / (56 GB/s pinned H2D / 4 B); never bench.py value\"}\n",
                 mode.c_str(), nt, hw, nch, n, ntaps, reps, rate, samples / best / 1e6, med * 1e3,
-                rate / (56e9 / 4.0 / 1e6), identical ? "true" : "false", (double)st.calls / reps,
+                rate / (56e9 / 4.0 / 1e6), samples / (fanout_s / reps) / 1e6,
+                samples / (fanout_s / reps) / 1e6 / (56e9 / 4.0 / 1e6), alloc_s / reps * 1e3, fanout_s / reps * 1e3,
+                identical ? "true" : "false", (double)st.calls / reps,
                 st.calls ? (double)st.staged_calls / (double)st.calls : 0.0,
                 (double)(st.h2d_bytes + st.d2h_bytes) / reps / med / 1e9, sp.wall_ms / calls, sp.h2d_ms / calls,
                 sp.kernel_ms / calls, sp.d2h_ms / calls, sp.h2d_ms / (tprof * 1e3), sp.kernel_ms / (tprof * 1e3),

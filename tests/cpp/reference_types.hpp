@@ -10,9 +10,62 @@
 #include <atomic>
 #include <cmath>
 #include <cstddef>
+#include <cstdlib>
+#include <mutex>
+#include <new>
+#include <set>
 #include <vector>
 
+#include "lcfir.h"
+
 namespace Diskerror {
+
+// Where the stand-in VectorMath keeps its samples: pageable memory (the
+// default, as c_lib's std::vector-backed type would) or, for
+// tests/cpp/dropin_bench --pinned, page-locked memory from lcfir_host_malloc
+// (a host that pins its buffers; lcfir_apply_range then DMAs them directly).
+inline bool &vectormath_pinned() {
+    static bool pinned = false;
+    return pinned;
+}
+struct PinnedBlocks { // the blocks lcfir_host_malloc gave out (freed by lcfir_host_free)
+    std::mutex mu;
+    std::set<void *> live;
+    static PinnedBlocks &get() {
+        static PinnedBlocks *b = new PinnedBlocks;
+        return *b;
+    }
+};
+template <class T>
+struct SampleAlloc {
+    using value_type = T;
+    SampleAlloc() = default;
+    template <class U>
+    SampleAlloc(const SampleAlloc<U> &) {}
+    T *allocate(size_t n) {
+        void *p = nullptr;
+        if (vectormath_pinned()) {
+            if (lcfir_host_malloc(n * sizeof(T), &p) != LCFIR_OK) throw std::bad_alloc();
+            std::lock_guard<std::mutex> lk(PinnedBlocks::get().mu);
+            PinnedBlocks::get().live.insert(p);
+        } else if (!(p = std::malloc(n * sizeof(T)))) {
+            throw std::bad_alloc();
+        }
+        return static_cast<T *>(p);
+    }
+    void deallocate(T *p, size_t) {
+        {
+            std::lock_guard<std::mutex> lk(PinnedBlocks::get().mu);
+            if (PinnedBlocks::get().live.erase(p)) {
+                lcfir_host_free(p);
+                return;
+            }
+        }
+        std::free(p);
+    }
+    bool operator==(const SampleAlloc &) const { return true; }
+    bool operator!=(const SampleAlloc &) const { return false; }
+};
 
 template <class T>
 class VectorMath {
@@ -20,8 +73,8 @@ public:
     VectorMath() = default;
     explicit VectorMath(size_t n) : v_(n) {}
     size_t size() const { return v_.size(); }
-    typename std::vector<T>::const_iterator begin() const { return v_.begin(); }
-    typename std::vector<T>::iterator begin() { return v_.begin(); }
+    typename std::vector<T, SampleAlloc<T>>::const_iterator begin() const { return v_.begin(); }
+    typename std::vector<T, SampleAlloc<T>>::iterator begin() { return v_.begin(); }
     T &operator[](size_t i) { return v_[i]; }
     const T &operator[](size_t i) const { return v_[i]; }
     T max_mag() const {
@@ -31,7 +84,7 @@ public:
     }
 
 private:
-    std::vector<T> v_;
+    std::vector<T, SampleAlloc<T>> v_;
 };
 
 // fms semantics as FilterCore.h calls it: fms(p) = all taps,

@@ -102,19 +102,21 @@ BENCH = os.path.join(ROOT, "tests", "cpp", "dropin_bench")
 
 def test_dropin_bench_short(dropin):
     """tests/cpp/dropin_bench (the drop-in's timing tool, profiles/) on a 4-s
-    stereo file: both staging modes, 1 and 5 threads, every file bit-identical
-    to the one-launch device call, the stats and the per-call split filled."""
+    stereo file: both staging modes and pinned caller buffers, 1 and 5
+    threads, every file bit-identical to the one-launch device call, the stats
+    and the per-call split filled."""
     import json
     r = subprocess.run([BENCH, "--seconds", "4", "--threads", "1,5", "--reps", "1"],
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr + r.stdout
     lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
-    assert [(d["mode"], d["threads"]) for d in lines] == [("bounce", 1), ("bounce", 5), ("pageable", 1),
-                                                          ("pageable", 5)]
+    assert [(d["mode"], d["threads"]) for d in lines] == [(m, t) for m in ("pageable", "bounce", "pinned")
+                                                          for t in (1, 5)]
     for d in lines:
         assert d["bit_identical"] is True and d["msamples_per_s"] > 0 and d["ntaps"] == 4001
         assert d["calls_per_file"] == 2 * d["threads"]
         assert d["staged_calls_frac"] == (1.0 if d["mode"] == "bounce" else 0.0)
+        assert d["fanout_msamples_per_s"] >= d["msamples_per_s"] and d["alloc_ms_per_file"] >= 0
         sp = d["split_per_call_ms"]
         assert sp["kernel"] > 0 and sp["h2d"] > 0 and sp["d2h"] > 0 and sp["wall"] > 0
 
@@ -163,7 +165,7 @@ def test_apply_range_staging_modes(oracle_mod, mode):
             lib.lcfir_host_free(px)
             lib.lcfir_host_free(py)
     finally:
-        lcfir.staging_set_mode("bounce")
+        lcfir.staging_set_mode("pageable")  # the library's default
     idx = np.r_[np.arange(0, 20), np.arange(n - 20, n), np.arange(1000, n, 100_003)]
     ref, _ = oracle_mod.filter_points(x, taps, idx, oracle_mod.MODE_LD)
     d = want[idx].astype(np.float64) - ref
