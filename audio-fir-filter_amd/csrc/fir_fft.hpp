@@ -101,7 +101,10 @@ constexpr int kVmcnt0 = 0x0F70;     // s_waitcnt vmcnt(0) (expcnt, lgkmcnt left 
 // written once and every workgroup stores its segment in the same phase; nt
 // stores drain that burst faster (+5 % on config 2; nt, sc0 or sc1 on the
 // sample loads measured 0 to -5 %, so those stay cached)
-constexpr int kNtStore = 2;
+#ifndef LCFIR_FFT_STORE_AUX
+#define LCFIR_FFT_STORE_AUX 2
+#endif
+constexpr int kNtStore = LCFIR_FFT_STORE_AUX;
 // output modes of fir_fft_f64_kernel (see there)
 constexpr int kFftOutF32 = 0, kFftOutFirst = 1, kFftOutAdd = 2, kFftOutLast = 3, kFftOutSym = 4;
 // kFftOutSym = kFftOutF32 for a linear-phase filter in zero-phase form: real

@@ -22,10 +22,15 @@ namespace Diskerror {
 
 // Where the stand-in VectorMath keeps its samples: pageable memory (the
 // default, as c_lib's std::vector-backed type would) or, for
-// tests/cpp/dropin_bench --pinned, page-locked memory from lcfir_host_malloc
-// (a host that pins its buffers; lcfir_apply_range then DMAs them directly).
+// tests/cpp/dropin_bench's pinned mode, page-locked memory from
+// lcfir_host_malloc (a host that pins its sample buffers; lcfir_apply_range
+// then DMAs them directly).  Per thread: the buffers the ProcessFile loop's
+// own thread makes (channels, temp_output) follow it, while the small
+// VectorMath temporaries the drop-in builds on the worker threads (the tap
+// fingerprint window) stay pageable -- a pinned allocation per call costs
+// ~0.3 ms of driver time.
 inline bool &vectormath_pinned() {
-    static bool pinned = false;
+    static thread_local bool pinned = false;
     return pinned;
 }
 struct PinnedBlocks { // the blocks lcfir_host_malloc gave out (freed by lcfir_host_free)

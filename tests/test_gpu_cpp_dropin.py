@@ -121,14 +121,15 @@ def test_dropin_bench_short(dropin):
         assert sp["kernel"] > 0 and sp["h2d"] > 0 and sp["d2h"] > 0 and sp["wall"] > 0
 
 
-@pytest.mark.parametrize("mode", ["bounce", "pageable"])
-def test_apply_range_staging_modes(oracle_mod, mode):
+@pytest.mark.parametrize("mode,ntaps", [("bounce", 4001), ("pageable", 4001), ("pageable", 41)])
+def test_apply_range_staging_modes(oracle_mod, mode, ntaps):
     """lcfir_apply_range through each staging mode and from pinned host
     memory (copied directly): ranges that span several 4 MiB bounce chunks,
-    odd sizes and one-sample ranges, all equal to the device call's bytes."""
+    odd sizes and one-sample ranges, all equal to the device call's bytes
+    (FFT at 4 001 taps, the direct form at 41)."""
     import lcfir
     import synth
-    taps = oracle_mod.design_lowcut(20.0, 48000.0, 4001)
+    taps = oracle_mod.design_lowcut(20.0, 48000.0, ntaps)
     n = 3_000_001
     x = np.ascontiguousarray(synth.file_buffer(1, n, 48000.0, file=31, bits=24)[0])
     flt = lcfir.Filter(taps)
