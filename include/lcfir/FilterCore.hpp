@@ -197,6 +197,11 @@ bool direct_taps_valid(const Sinc &sinc, const double *h, size_t T) {
     return true;
 }
 
+// Entries of the per-object sinc caches below: the reference builds one
+// WindowedSinc per file, usually at the same address, so a few suffice; past
+// the cap a cache starts over instead of growing with every object seen.
+constexpr size_t kSincCacheCap = 64;
+
 template <class Channel, class Sinc>
 std::shared_ptr<const std::vector<double>> probe_taps(const Sinc &sinc) {
     const int64_t half = (int64_t)sinc.getMo2();
@@ -216,6 +221,7 @@ std::shared_ptr<const std::vector<double>> probe_taps(const Sinc &sinc) {
     if (it != cache->end() && it->second.half == half &&
         std::memcmp(&it->second.finger, &finger, sizeof finger) == 0)
         return it->second.taps;
+    if (cache->size() >= kSincCacheCap && !cache->count(&sinc)) cache->clear(); // bounded: sinc objects come and go
     Channel imp((size_t)(2 * T - 1));
     for (int64_t i = 0; i < 2 * T - 1; ++i) imp[(size_t)i] = 0.0f;
     imp[(size_t)(T - 1)] = 1.0f;
@@ -289,6 +295,7 @@ std::shared_ptr<Filter> direct_filter(const Sinc &sinc, const double *h, size_t 
     if (!direct_taps_valid<Channel>(sinc, h, T)) return nullptr;
     auto flt = FilterCache::instance().get(h, T, device);
     std::lock_guard<std::mutex> lk(mu);
+    if (cache->size() >= kSincCacheCap && !cache->count(&sinc)) cache->clear(); // bounded: sinc objects come and go
     (*cache)[&sinc] = Entry{h, T, device, std::vector<double>(h, h + T), flt};
     return flt;
 }
