@@ -233,6 +233,8 @@ std::shared_ptr<const std::vector<double>> probe_taps(const Sinc &sinc) {
 } // namespace detail
 
 // ---- per-process filter cache (one upload per tap set and device) -------------
+// Bounded like the sinc caches: past kCap distinct tap sets the map starts over
+// (a Filter still in use elsewhere lives on through its shared_ptr).
 class FilterCache {
 public:
     static FilterCache &instance() {
@@ -246,6 +248,7 @@ public:
         auto it = map_.find(key);
         if (it != map_.end()) return it->second;
         auto f = std::make_shared<Filter>(taps, (int32_t)ntaps, device);
+        if (map_.size() >= kCap) map_.clear();
         map_.emplace(std::move(key), f);
         return f;
     }
@@ -253,6 +256,12 @@ public:
         std::lock_guard<std::mutex> lk(mu_);
         map_.clear();
     }
+
+    size_t size() {
+        std::lock_guard<std::mutex> lk(mu_);
+        return map_.size();
+    }
+    static constexpr size_t kCap = 16;
 
 private:
     std::mutex mu_;

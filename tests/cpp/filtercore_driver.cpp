@@ -6,7 +6,10 @@
 //
 // usage: filtercore_driver in.f32 taps.f64 out.f32 nch n threads mode normalize
 //        mode 0 = process_buffer (threaded hand-off), 1 = process_buffer_device,
-//        2 / 3 = process_buffer with a PaddedSinc / ReversedSinc
+//        2 / 3 = process_buffer with a PaddedSinc / ReversedSinc,
+//        4 / 5 = a WindowedSinc / PaddedSinc first used with other taps (half
+//        of them), then rewritten in place (same object, same data() pointer):
+//        the drop-in's per-object caches must miss on the second file
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
@@ -94,6 +97,22 @@ int main(int argc, char **argv) {
             const std::vector<double> taps = lcfir::sinc_taps<std::vector<float>>(sinc);
             lcfir::Filter flt(taps.data(), (int32_t)taps.size());
             peak = lcfir::process_buffer_device(buf, flt, opts);
+        } else if (mode == 4 || mode == 5) {
+            std::vector<double> half(sinc.k);
+            for (double &v : half) v *= 0.5;
+            WindowedSinc ws{half};
+            PaddedSinc ps(half);
+            const double *before = mode == 4 ? ws.data() : ps.data();
+            auto first = buf;  // the earlier file
+            if (mode == 4) lcfir::process_buffer(first, ws, opts, &prog);
+            else lcfir::process_buffer(first, ps, opts, &prog);
+            for (double &v : ws.k) v *= 2.0;  // exact: the real taps, in place
+            for (double &v : ps.h) v *= 2.0;
+            for (double &v : ps.padded) v *= 2.0;
+            if (before != (mode == 4 ? ws.data() : ps.data())) { std::fprintf(stderr, "moved\n"); return 3; }
+            prog.count = 0;
+            peak = mode == 4 ? lcfir::process_buffer(buf, ws, opts, &prog) : lcfir::process_buffer(buf, ps, opts, &prog);
+            if (prog.count != nch * n) { std::fprintf(stderr, "progress %zu\n", prog.count); return 3; }
         } else if (mode == 2) {
             peak = lcfir::process_buffer(buf, PaddedSinc(sinc.k), opts, &prog);
         } else {

@@ -35,11 +35,14 @@ def run(driver, tmp_path, x, taps, threads, mode, normalize):
 
 @pytest.mark.parametrize("threads,mode,normalize", [(1, 0, False), (4, 0, False), (7, 0, True),
                                                     (1, 1, False), (1, 1, True), (3, 2, False),
-                                                    (3, 3, False)])
+                                                    (3, 3, False), (4, 4, False), (4, 5, True)])
 def test_cpp_process_buffer(driver, tmp_path, oracle_mod, threads, mode, normalize):
     """Modes 2 and 3: a sinc whose data()/size() are not the fms() kernel
     (padded / reversed; the random_int24 taps are asymmetric) -- the drop-in
-    must fall back to recovering the taps through fms()."""
+    must fall back to recovering the taps through fms().  Modes 4 and 5: the
+    sinc object is rewritten in place between two files (same address, same
+    data() pointer, other taps), through the direct and the fms() path -- the
+    second file must use the new taps."""
     g = load_golden("random_int24")
     taps = g["taps"]
     if mode == 3:  # visibly asymmetric, so reversed taps filter differently
