@@ -151,6 +151,7 @@ struct FftPlan {
     uint32_t *d_task = nullptr; // [halves][512] task words (cA, d1A, e1A, cB, d1B, e1B)
     int cus = 256;             // compute units of the plan's device (persistent grid)
     bool sym = false;          // linear-phase filter run in zero-phase form (kFftOutSym)
+    bool reg32 = false;        // L = 32768 zero-phase on the register-resident kernel (fir_fft32r.hpp)
     FftTuning tune;            // the ctx's tuning when the plan was built
 };
 
@@ -206,8 +207,16 @@ inline int fft_partition_count(int ntaps, int L = 16384) {
 // partial sums; an L = 32 768 unit is two 8192-point halves plus the split,
 // the merge and the park slab, the general pair table and partitions cost
 // more there (register pressure).
+#ifndef LCFIR_FFT32R
+#define LCFIR_FFT32R 0 // 1: zero-phase single-partition L = 32768 plans run fir_fft32r_kernel
+#endif
+#ifndef LCFIR_FFT32R_COST
+#define LCFIR_FFT32R_COST 2.9
+#endif
+inline bool fft_reg32(int L, int parts, bool sym) { return LCFIR_FFT32R && L == 32768 && parts == 1 && sym; }
 inline double fft_unit_cost(int L, int parts, bool sym) {
     if (L == 16384) return parts == 1 ? 1.0 : 1.25;
+    if (fft_reg32(L, parts, sym)) return LCFIR_FFT32R_COST;
     return parts == 1 ? (sym ? 2.9 : 3.1) : 4.0;
 }
 // Estimated time per output with segment length L: partitions x unit cost /
@@ -394,11 +403,62 @@ __device__ __forceinline__ void dft4_r2(double2 &a0, double2 &a1, double2 u2, do
     a3 = csub(t1, t3);
 }
 
+#ifndef LCFIR_FFT_DFT16F
+#define LCFIR_FFT_DFT16F 0
+#endif
+constexpr double kT1 = 0.41421356237309504880; // tan(pi/8)
+// W16^1, W16^3 and W16^9 are cos(pi/8) times (1 - i tan), -i (1 + i tan) and
+// -(1 - i tan): the rotations by tan are two FMAs each (no MUL) and the common
+// cos(pi/8) stays pending into the row's radix-4, whose last adds become FMAs.
+__device__ __forceinline__ double2 rot16_1(double2 a) { // a W16^1 / kC1
+    return make_double2(__builtin_fma(kT1, a.y, a.x), __builtin_fma(-kT1, a.x, a.y));
+}
+__device__ __forceinline__ double2 rot16_3(double2 a) { // a W16^3 / kC1
+    return make_double2(__builtin_fma(kT1, a.x, a.y), __builtin_fma(kT1, a.y, -a.x));
+}
+__device__ __forceinline__ double2 rot16_9(double2 a) { // a W16^9 / kC1
+    return make_double2(__builtin_fma(-kT1, a.y, -a.x), __builtin_fma(kT1, a.x, -a.y));
+}
+// dft4(a0, a1, a2, a3) for a1 = kC1 p1, a2 = kR2 u2, a3 = kC1 p3
+__device__ __forceinline__ void dft4_r2c(double2 &a0, double2 p1, double2 u2, double2 &a2, double2 p3,
+                                         double2 &o1, double2 &o3) {
+    double2 t0, t1;
+    fma_pm(a0, u2, t0, t1);
+    const double2 s = cadd(p1, p3), d = csub(p1, p3);
+    a0 = make_double2(__builtin_fma(kC1, s.x, t0.x), __builtin_fma(kC1, s.y, t0.y));
+    a2 = make_double2(__builtin_fma(-kC1, s.x, t0.x), __builtin_fma(-kC1, s.y, t0.y));
+    // t3 = -i kC1 d
+    o1 = make_double2(__builtin_fma(kC1, d.y, t1.x), __builtin_fma(-kC1, d.x, t1.y));
+    o3 = make_double2(__builtin_fma(-kC1, d.y, t1.x), __builtin_fma(kC1, d.x, t1.y));
+}
+
 // forward 16-point DFT, natural order in and out (4 x 4 Cooley-Tukey)
 __device__ __forceinline__ void dft16(double2 (&a)[16]) {
     // radix-4 over n1 for each n2: slot 4*n1 + n2 -> slot 4*k1 + n2
 #pragma unroll
     for (int n2 = 0; n2 < 4; ++n2) dft4(a[n2], a[4 + n2], a[8 + n2], a[12 + n2]);
+#if LCFIR_FFT_DFT16F
+    a[10] = w16<4>(a[10]);
+    dft4(a[0], a[1], a[2], a[3]);
+    {
+        double2 o1, o3; // row 1: (a4, kC1 rot16_1(a5), kR2 rot8_1(a6), kC1 rot16_3(a7))
+        dft4_r2c(a[4], rot16_1(a[5]), rot8_1(a[6]), a[6], rot16_3(a[7]), o1, o3);
+        a[5] = o1;
+        a[7] = o3;
+    }
+    {
+        double2 o1, o3; // row 2: (a8, kR2 rot8_1(a9), -i a10, kR2 rot8_3(a11))
+        dft4_r13(a[8], rot8_1(a[9]), a[10], rot8_3(a[11]), o1, o3);
+        a[9] = o1;
+        a[11] = o3;
+    }
+    {
+        double2 o1, o3; // row 3: (a12, kC1 rot16_3(a13), kR2 rot8_3(a14), kC1 rot16_9(a15))
+        dft4_r2c(a[12], rot16_3(a[13]), rot8_3(a[14]), a[14], rot16_9(a[15]), o1, o3);
+        a[13] = o1;
+        a[15] = o3;
+    }
+#else
     // twiddles W16^(n2*k1), slot 4*k1 + n2, then radix-4 over n2 for each k1:
     // slot 4*k1 + k2 holds X[k1 + 4*k2].  The W16^2 = W8^1 and W16^6 = W8^3
     // rotations keep their sqrt(1/2) pending into the radix-4 (dft4_r13 and
@@ -418,6 +478,7 @@ __device__ __forceinline__ void dft16(double2 (&a)[16]) {
         a[11] = o3;
     }
     dft4_r2(a[12], a[13], rot8_3(a[14]), a[14], a[15]); // row 3: (a12, a13 w3, kR2 rot8_3(a14), a15 w9)
+#endif
     double2 t[16];
 #pragma unroll
     for (int k1 = 0; k1 < 4; ++k1)
@@ -467,6 +528,25 @@ __device__ __forceinline__ void twiddle16(double2 (&a)[16], double2 w1) {
     a[15] = cmul(a[15], cmul(wo, w2));
 }
 
+#ifndef LCFIR_FFT_CHEB
+#define LCFIR_FFT_CHEB 0
+#endif
+#if LCFIR_FFT_CHEB
+// w[r] = w1^r for a unit w1, r = 1..15, by the Chebyshev recurrence
+// w^(r+2) = 2 Re(w^2) w^r - w^(r-2): two FMAs per power instead of a complex
+// multiply's two MULs and two FMAs; odd and even powers in two chains of depth 7
+__device__ __forceinline__ void powers16(double2 w1, double2 (&w)[16]) {
+    const double c2 = w1.x + w1.x;
+    w[1] = w1;
+    w[2] = make_double2(__builtin_fma(c2, w1.x, -1.0), c2 * w1.y);
+    const double q2 = w[2].x + w[2].x;
+    w[3] = make_double2(__builtin_fma(c2, w[2].x, -w1.x), __builtin_fma(c2, w[2].y, -w1.y));
+    w[4] = make_double2(__builtin_fma(q2, w[2].x, -1.0), q2 * w[2].y);
+#pragma unroll
+    for (int r = 5; r < 16; ++r)
+        w[r] = make_double2(__builtin_fma(q2, w[r - 2].x, -w[r - 4].x), __builtin_fma(q2, w[r - 2].y, -w[r - 4].y));
+}
+#else
 // w[r] = w1^r, r = 1..15, by twiddle16's chain (the same values, bit for bit)
 __device__ __forceinline__ void powers16(double2 w1, double2 (&w)[16]) {
     const double2 w2 = cmul(w1, w1);
@@ -479,12 +559,27 @@ __device__ __forceinline__ void powers16(double2 w1, double2 (&w)[16]) {
     }
     w[15] = cmul(w[13], w2);
 }
+#endif
 
 __device__ __forceinline__ void apply16(double2 (&a)[16], const double2 (&w)[16]) {
 #pragma unroll
     for (int r = 1; r < 16; ++r) a[r] = cmul(a[r], w[r]);
 }
 
+#if LCFIR_FFT_CHEB
+// w[r] = w1^r, r = 1..7 (powers16's recurrence, depth 4)
+__device__ __forceinline__ void powers8(double2 w1, double2 (&w)[8]) {
+    const double c2 = w1.x + w1.x;
+    w[1] = w1;
+    w[2] = make_double2(__builtin_fma(c2, w1.x, -1.0), c2 * w1.y);
+    const double q2 = w[2].x + w[2].x;
+    w[3] = make_double2(__builtin_fma(c2, w[2].x, -w1.x), __builtin_fma(c2, w[2].y, -w1.y));
+    w[4] = make_double2(__builtin_fma(q2, w[2].x, -1.0), q2 * w[2].y);
+#pragma unroll
+    for (int r = 5; r < 8; ++r)
+        w[r] = make_double2(__builtin_fma(q2, w[r - 2].x, -w[r - 4].x), __builtin_fma(q2, w[r - 2].y, -w[r - 4].y));
+}
+#else
 // w[r] = w1^r, r = 1..7 (depth <= 3)
 __device__ __forceinline__ void powers8(double2 w1, double2 (&w)[8]) {
     w[1] = w1;
@@ -495,6 +590,7 @@ __device__ __forceinline__ void powers8(double2 w1, double2 (&w)[8]) {
     w[6] = cmul(w[4], w[2]);
     w[7] = cmul(w[4], w[3]);
 }
+#endif
 
 __device__ __forceinline__ void twiddle8(double2 (&a)[8], const double2 (&w)[8]) {
 #pragma unroll
@@ -1213,6 +1309,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
 }
 
 #include "fir_fft32.hpp"
+#include "fir_fft32r.hpp"
 
 // ---------------------------------------------------------------------------
 // host side
@@ -1257,12 +1354,81 @@ inline void fft_ld(std::vector<long double> &re, std::vector<long double> &im) {
 // test that runs scripts/fft32_model.py's emulation of the kernel on them.
 struct FftTables {
     int L = 0, halves = 1, parts = 1, tp = 0;
-    bool sym = false;
+    bool sym = false, reg32 = false;
     std::vector<double2> pair; // parts x halves x kFftPairTable
     std::vector<uint32_t> task; // halves x 512
     std::vector<double2> c8;   // per partition
     std::vector<double2> tw;   // kFftTw or kFft32Tw
 };
+
+// fir_fft32r_kernel's tables (zero-phase, one partition, L = 32768): per
+// thread t and pair slot i the zero-phase coefficients p1, q2, p2 of the bin in
+// its R1 register i (the special lane: of its permuted x' list), the task
+// words, and the twiddles W_16384^b, W_1024^b (b < 512), W_512^g (g < 16).
+inline void r32_plan_tables(const std::vector<double> &taps, FftTables &T) {
+    const int ntaps = (int)taps.size(), L = kFft32L, N = L / 2;
+    const long double scale = 1.0L / (4.0L * (long double)N);
+    const long double two_pi = 6.283185307179586476925286766559L;
+    std::vector<long double> re((size_t)L, 0.0L), im((size_t)L, 0.0L);
+    const int half = (ntaps - 1) / 2;
+    for (int j = -half; j <= half; ++j)
+        re[(size_t)((j + L) % L)] =
+            ((long double)taps[(size_t)(half + j)] + (long double)taps[(size_t)(half - j)]) * 0.5L;
+    detail::fft_ld(re, im);
+    // p1, q2, p2 of bin k (fft_pair_sym; fft_plan_tables' zero-phase layout)
+    auto coef = [&](int k, long double &p1, long double &q2, long double &p2, long double &c8v) {
+        const long double gr = re[(size_t)k] * scale, hr = re[(size_t)(N - k)] * scale;
+        const long double sr = gr + hr, dr = gr - hr;
+        const long double a = -two_pi * (long double)k / (long double)L;
+        p1 = 2 * sr + 2 * dr * sinl(a);
+        q2 = 2 * sr - 2 * dr * sinl(a);
+        p2 = 2 * dr * cosl(a);
+        c8v = 2 * sr - 2 * dr;
+    };
+    T.pair.assign(kR32PairTable, make_double2(0.0, 0.0));
+    T.task.resize(kFftNT);
+    for (int t = 0; t < kFftNT; ++t) {
+        T.task[(size_t)t] = r32_task_word(t);
+        int bx[16], by[16];
+        r32_task_bins(t, bx, by);
+        if (t == kR32SpecialLane) {
+            // x' = [R2 0..7, R1 1..7, R1 0] (fir_fft32r_kernel's permutation)
+            int px[16];
+            for (int i = 0; i < 8; ++i) px[i] = by[i];
+            for (int i = 8; i < 15; ++i) px[i] = bx[i - 7];
+            px[15] = bx[0];
+            for (int i = 0; i < 16; ++i) bx[i] = px[i];
+        }
+        for (int i = 0; i < 16; ++i) {
+            long double p1, q2, p2, c8v;
+            coef(bx[i], p1, q2, p2, c8v);
+            T.pair[(size_t)i * kFftNT + (size_t)t] = make_double2((double)p1, (double)q2);
+            double *p2t = reinterpret_cast<double *>(&T.pair[(size_t)(16 + (i >> 1)) * kFftNT + (size_t)t]);
+            p2t[i & 1] = (double)p2;
+        }
+    }
+    {
+        long double p1, q2, p2, c8v;
+        coef(N / 2, p1, q2, p2, c8v);
+        T.c8.assign(1, make_double2((double)c8v, 0.0));
+    }
+    T.tw.resize(kR32Tw);
+    for (int b = 0; b < 512; ++b) {
+        const long double a = -two_pi * (long double)b / 16384.0L, a16 = -two_pi * (long double)b / 1024.0L;
+        T.tw[(size_t)(kR32TwB + b)] = make_double2((double)cosl(a), (double)sinl(a));
+        T.tw[(size_t)(kR32TwB16 + b)] = make_double2((double)cosl(a16), (double)sinl(a16));
+    }
+    for (int g = 0; g < 16; ++g) {
+        const long double a = -two_pi * (long double)g / 512.0L;
+        T.tw[(size_t)(kR32TwG + g)] = make_double2((double)cosl(a), (double)sinl(a));
+    }
+    T.L = L;
+    T.halves = 1;
+    T.parts = 1;
+    T.tp = ntaps;
+    T.sym = true;
+    T.reg32 = true;
+}
 
 inline FftTables fft_plan_tables(const std::vector<double> &taps, const FftTuning &tune) {
     const int ntaps = (int)taps.size();
@@ -1286,6 +1452,10 @@ inline FftTables fft_plan_tables(const std::vector<double> &taps, const FftTunin
     FftTables T;
     std::vector<double2> &pair = T.pair, &c8 = T.c8;
     std::vector<uint32_t> &task = T.task;
+    if (fft_reg32(L, parts, sym)) {
+        r32_plan_tables(taps, T);
+        return T;
+    }
     pair.resize((size_t)parts * halves * kFftPairTable);
     task.resize((size_t)halves * kFftNT);
     c8.resize((size_t)parts);
@@ -1414,6 +1584,7 @@ inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, const
     plan.ntaps = T.tp;
     plan.parts = T.parts;
     plan.sym = T.sym;
+    plan.reg32 = T.reg32;
     plan.tune = tune;
     plan.B = T.L - T.tp + 1;
     plan.c8 = T.c8;
@@ -1437,9 +1608,34 @@ inline int64_t fft_chunk(const FftPlan &plan) {
     return plan.tune.chunk >= 4096 ? plan.tune.chunk : ((int64_t)1 << 28);
 }
 
+// work array + twiddles + 8 f32 peak slots + the special lane's 32 double2
+constexpr size_t kR32LdsBytes = sizeof(double2) * (size_t)(kFftM + kR32Tw + 2 + 32);
+
+template <int kOut>
+inline bool fft32r_launch_one(const FftPlan &plan, const DirectParams &q, int nch, hipStream_t s, std::string &err) {
+    static const bool attr = [] {
+        return hipFuncSetAttribute(reinterpret_cast<const void *>(&fir_fft32r_kernel<kOut>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kR32LdsBytes) == hipSuccess;
+    }();
+    (void)attr;
+    const int64_t nseg = (q.end - q.seg0 + plan.B - 1) / plan.B;
+    const int64_t units = nseg * nch; // < 2^31 (fft_launch)
+    const int64_t grid = std::min<int64_t>(units, (int64_t)plan.cus);
+    hipLaunchKernelGGL(fir_fft32r_kernel<kOut>, dim3((unsigned)grid), dim3(kFftNT), kR32LdsBytes, s, q, plan.d_pair,
+                       plan.d_tw, plan.d_task, plan.B, fft_grid(nseg, units), plan.c8[0].x);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        err = hipGetErrorString(e);
+        return false;
+    }
+    return true;
+}
+
 template <int kOut>
 inline bool fft32_launch_one(const FftPlan &plan, const DirectParams &q, int part, int nch, hipStream_t s,
                              std::string &err) {
+    if constexpr (kOut == kFftOutSym)
+        if (plan.reg32) return fft32r_launch_one<kOut>(plan, q, nch, s, err);
     static const bool attr = [] {
         return hipFuncSetAttribute(reinterpret_cast<const void *>(&fir_fft32_f64_kernel<kOut>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1545,7 +1741,7 @@ inline size_t fft_scratch_doubles(const FftPlan &plan, const DirectParams &p, in
 // Doubles of park slab an L = 32768 launch needs (one slab per workgroup of
 // the persistent grid, fir_fft32.hpp); launches on one stream reuse it.
 inline size_t fft32_park_doubles(const FftPlan &plan) {
-    return plan.L == kFft32L ? (size_t)plan.cus * kParkSlab * kFftNT * 2 : 0;
+    return plan.L == kFft32L && !plan.reg32 ? (size_t)plan.cus * kParkSlab * kFftNT * 2 : 0;
 }
 
 // Filter outputs [p.start, p.end) of nch channels.  p.half / p.ntaps are the

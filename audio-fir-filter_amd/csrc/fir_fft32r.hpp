@@ -1,0 +1,551 @@
+// fir_fft32r.hpp -- the L = 32 768 zero-phase overlap-save unit held in
+// registers ("L = 32 768 in registers").
+//
+// fir_fft32.hpp runs an L = 32 768 segment as two 8192-point halves through
+// fir_fft.hpp's column phase, parking the idle half in a global slab: 12 LDS
+// round trips of 128 KiB per segment, the same LDS bytes per transform point
+// as L = 16 384.  Here the 16 384-point complex transform stays in the
+// register file instead -- 32 complex f64 per thread, 256 KiB per workgroup,
+// half of the CU's VGPRs -- and the LDS only carries the exchanges, each in
+// two rounds of 128 KiB:
+//
+//   z[m] = x_seg[2m] + i x_seg[2m+1], m = 512 n + b (thread b, register n),
+//   b = 16 beta + gamma;   bins k = k1 + 32 kappa + 1024 lambda.
+//   stage 1 (thread b): DFT32 over n -> k1, * W_16384^(b k1)
+//   T1 (workgroup, 2 rounds): lane (k1, gamma) of column k1 gathers beta
+//   stage 2: DFT32 over beta -> kappa, * W_512^(gamma kappa)
+//   T2 (wave-local, 2 rounds): lane s of a 32-lane group gathers gamma for
+//       task R1 (column, kappa < 16) and task R2 (its mirror, kappa >= 16)
+//   stage 3: DFT16 over gamma -> lambda;  pair step R1[i] <-> R2[15 - i]
+//   (bins k and N - k), the zero-phase pair table; then stage 3, T2, stage 2,
+//   T1 and stage 1 again in reverse (the inverse as conj(FFT(conj(V)))).
+// Per segment: 4 exchanges (8 LDS rounds) of 256 KiB against fir_fft32.hpp's
+// 12 round trips of 128 KiB, 6 workgroup barriers, 3 radix stages per
+// direction instead of 4.
+//
+// Every register index is the same in every lane (no lane-dependent register
+// selection, which the compiler would lower through scratch):
+//   * round 1 of T1 carries the columns k1 < 16 of threads b < 256 and the
+//     columns k1 >= 16 of threads b >= 256.  Waves 4..7 negate their odd
+//     stage-1 inputs, which rotates their DFT32 outputs by 16 (register r
+//     holds k1 = r + 16 mod 32), so round 1 is registers 0..15 everywhere.
+//   * a column lane with k1 >= 16 (h = 1) receives beta rotated by 16; its
+//     DFT32 output picks up (-1)^kappa, folded into the twiddle base
+//     (-W_512^gamma instead of W_512^gamma).  The inverse stage 2 uses the same
+//     base, which rotates its outputs back into the round order.
+//   * the final DFT32 of waves 4..7 sees k1 rotated by 16: (-1)^n on its
+//     outputs, folded into the f32 stores' sign bits.
+// Wave 0's lane 31 holds the self-paired bins 0 and N/2 (tasks (0, 0) and
+// (0, 16)); it permutes its registers through a 512-B LDS scratch before and
+// after the pair step.  scripts/fft32r_model.py is the numpy model of this
+// flow (every register index, LDS slot and table slot; bank conflicts).
+//
+// Included by fir_fft.hpp after fir_fft32.hpp, inside namespace lcfir.
+
+constexpr int kR32TwB = 0;      // W_16384^b, b < 512
+constexpr int kR32TwB16 = 512;  // W_1024^b = W_16384^(16 b), b < 512
+constexpr int kR32TwG = 1024;   // W_512^g, g < 16
+constexpr int kR32Tw = 1024 + 16;
+constexpr size_t kR32PairTable = (size_t)24 * kFftNT; // double2: (p1, q2) [16][512], (p2 even, p2 odd) [8][512]
+constexpr int kR32SpecialLane = 31;                   // of wave 0
+#ifndef R32_SPECIAL
+#define R32_SPECIAL 1
+#endif
+
+// column k1 of lane (wave w, 32-lane group g, half h); mirror columns k1 and
+// 32 - k1 share a group (wave 0 group 0: the self-paired columns 0 and 16)
+__host__ __device__ constexpr int r32_column(int w, int g, int h) {
+    return w == 0 ? (g ? (h ? 24 : 8) : (h ? 16 : 0)) : (g ? (h ? 24 - w : w + 8) : (h ? 32 - w : w));
+}
+// 4 wave + 2 g + h of column k1 (the inverse of r32_column)
+__host__ __device__ constexpr int r32_column_home(int k1) {
+    return k1 == 0 ? 0 : k1 == 16 ? 1 : k1 == 8 ? 2 : k1 == 24 ? 3
+         : k1 < 8 ? 4 * k1 : k1 > 24 ? 4 * (32 - k1) + 1 : k1 < 16 ? 4 * (k1 - 8) + 2 : 4 * (24 - k1) + 3;
+}
+
+// Task word of thread t (host): T2's read tasks (h, kappa mod 16) for R1 (bits
+// 0..4) and R2 (bits 5..9), scripts/fft32r_model.py's t2_tasks
+inline uint32_t r32_task_word(int t) {
+    const int w = t >> 6, g = (t >> 5) & 1, s = t & 31;
+    int h1, k1, h2, k2;
+    if (w == 0 && g == 0) {
+        // column 16's tasks on read group {0-3, 12-15, 20-27}, column 0's and
+        // the special lane on {4-11, 16-19, 28-31}: conflict-free T2 reads
+        static const int ga[16] = {0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27};
+        static const int gb[15] = {4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30};
+        int ia = -1, ib = -1;
+        for (int i = 0; i < 16; ++i)
+            if (ga[i] == s) ia = i;
+        for (int i = 0; i < 15; ++i)
+            if (gb[i] == s) ib = i;
+        if (ia >= 0) {
+            h1 = 1, k1 = ia, h2 = 1, k2 = 31 - ia;
+        } else if (ib >= 0) {
+            h1 = 0, k1 = 1 + ib, h2 = 0, k2 = 31 - ib;
+        } else {
+            h1 = 0, k1 = 0, h2 = 0, k2 = 16; // the special lane
+        }
+    } else if (s < 16) {
+        h1 = 0, k1 = s, h2 = 1, k2 = 31 - s;
+    } else {
+        h1 = 1, k1 = 31 - s, h2 = 0, k2 = s;
+    }
+    return (uint32_t)(h1 | (k1 & 15) << 1 | h2 << 5 | (k2 & 15) << 6);
+}
+// bins of thread t's R1 / R2 registers lambda = 0..15 (host; pair tables)
+inline void r32_task_bins(int t, int (&bx)[16], int (&by)[16]) {
+    const int w = t >> 6, g = (t >> 5) & 1;
+    const uint32_t tk = r32_task_word(t);
+    const int cA = r32_column(w, g, tk & 1), kA = (tk >> 1) & 15;
+    const int cB = r32_column(w, g, (tk >> 5) & 1), kB = 16 + ((tk >> 6) & 15);
+    for (int l = 0; l < 16; ++l) {
+        bx[l] = cA + 32 * kA + 1024 * l;
+        by[l] = cB + 32 * kB + 1024 * l;
+    }
+}
+
+// forward 32-point DFT, natural order in and out (radix 2 x DFT16)
+__device__ __forceinline__ void dft32(double2 (&a)[32]) {
+    double2 e[16], o[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        e[r] = a[2 * r];
+        o[r] = a[2 * r + 1];
+    }
+    dft16(e);
+    dft16(o);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const double2 t = w32mul(o[k], k);
+        a[k] = cadd(e[k], t);
+        a[k + 16] = csub(e[k], t);
+    }
+}
+
+// a[off + r] *= s0 w^r, r < 16, for a unit w: s_{r+2} = 2 Re(w^2) s_r - s_{r-2}
+// (Chebyshev; two FMAs per power).  Each power is applied as it is made, so
+// only the last four are live.
+__device__ __forceinline__ void r32_chain16(double2 (&a)[32], int off, double2 s0, double2 w) {
+    const double c2 = w.x + w.x;
+    const double q2 = __builtin_fma(c2, c2, -2.0); // 2 Re(w^2)
+    double2 s1 = cmul(s0, w);
+    double2 s2 = make_double2(__builtin_fma(c2, s1.x, -s0.x), __builtin_fma(c2, s1.y, -s0.y));
+    double2 s3 = make_double2(__builtin_fma(c2, s2.x, -s1.x), __builtin_fma(c2, s2.y, -s1.y));
+    a[off] = cmul(a[off], s0);
+    a[off + 1] = cmul(a[off + 1], s1);
+    a[off + 2] = cmul(a[off + 2], s2);
+    a[off + 3] = cmul(a[off + 3], s3);
+#pragma unroll
+    for (int r = 4; r < 16; r += 2) {
+        const double2 n0 = make_double2(__builtin_fma(q2, s2.x, -s0.x), __builtin_fma(q2, s2.y, -s0.y));
+        const double2 n1 = make_double2(__builtin_fma(q2, s3.x, -s1.x), __builtin_fma(q2, s3.y, -s1.y));
+        a[off + r] = cmul(a[off + r], n0);
+        a[off + r + 1] = cmul(a[off + r + 1], n1);
+        s0 = s2;
+        s1 = s3;
+        s2 = n0;
+        s3 = n1;
+    }
+}
+// a[r] *= w^r, r < 32 (r = 0 untouched), the same recurrence
+__device__ __forceinline__ void r32_chain32(double2 (&a)[32], double2 w) {
+    const double c2 = w.x + w.x;
+    const double q2 = __builtin_fma(c2, c2, -2.0);
+    double2 s0 = make_double2(1.0, 0.0), s1 = w;
+    double2 s2 = make_double2(__builtin_fma(c2, w.x, -1.0), c2 * w.y);
+    double2 s3 = make_double2(__builtin_fma(c2, s2.x, -w.x), __builtin_fma(c2, s2.y, -w.y));
+    a[1] = cmul(a[1], s1);
+    a[2] = cmul(a[2], s2);
+    a[3] = cmul(a[3], s3);
+#pragma unroll
+    for (int r = 4; r < 32; r += 2) {
+        const double2 n0 = make_double2(__builtin_fma(q2, s2.x, -s0.x), __builtin_fma(q2, s2.y, -s0.y));
+        const double2 n1 = make_double2(__builtin_fma(q2, s3.x, -s1.x), __builtin_fma(q2, s3.y, -s1.y));
+        a[r] = cmul(a[r], n0);
+        a[r + 1] = cmul(a[r + 1], n1);
+        s0 = s2;
+        s1 = s3;
+        s2 = n0;
+        s3 = n1;
+    }
+}
+
+// Samples of unit (ch, n0) into wave w's region flds[1024 w, + 1024) as the
+// float2 z[512 n + 64 w + i] at float2 index 2048 w + 64 n + i (the caller
+// has retired the wave's reads of its region).  Interior units by LDS-DMA
+// (16 b128 transfers per lane, no VGPRs); edge units through fft_load_unit's
+// range-checked loads.
+__device__ __forceinline__ void r32_stage_samples(const DirectParams &p, int ch, int64_t n0, int j, double2 *flds) {
+    const int w = j >> 6, lane = j & 63;
+    const float *x = p.x + (int64_t)ch * p.x_stride;
+    const int64_t w0 = n0 - p.half - p.x_lo;
+    if (w0 >= 0 && w0 + kFft32L <= p.x_hi - p.x_lo) {
+        const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float *>(x), (short)0, (int)((p.x_hi - p.x_lo) * 4), 0x00020000);
+        // transfer s, lane l: z[512 n + 64 w + 2k], z[.. + 1], n = 2s + (l >> 5),
+        // k = l & 31 (the 16 bytes at 4 w0 + 8192 s + 4096 (l >> 5) + 512 w + 16 k)
+        // into LDS byte 16384 w + 1024 s + 16 l (float2 2048 w + 64 n + 2k)
+        const int vofs = 4096 * (lane >> 5) + 512 * w + 16 * (lane & 31);
+        const int sofs = (int)(w0 * 4);
+#pragma unroll
+        for (int s = 0; s < 16; ++s)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (fft_lds_void *)(flds + 1024 * w + 64 * s), 16, vofs,
+                                                     sofs + 8192 * s, 0, 0);
+    } else {
+        float2 v[32];
+        fft_load_unit<32>(p, ch, n0, j, v);
+        float2 *fz = reinterpret_cast<float2 *>(flds) + 2048 * w + lane;
+#pragma unroll
+        for (int n = 0; n < 32; ++n) fz[64 * n] = v[n];
+    }
+}
+
+// Outputs of one unit: c[2m] = Re out[n], c[2m+1] = -Im out[n], m = j + 512 n,
+// valid for c in [half, L - half); sg = the sign bit waves 4..7 put on odd n
+// (their rotated final DFT32).  Range-checked buffer stores, nt, as
+// fir_fft32.hpp's fft32_store_unit (quad form when half is a multiple of 4).
+__device__ __forceinline__ float r32_store_unit(const DirectParams &p, int ch, int64_t n0, int B, int j,
+                                                const double2 (&o)[32], int sg) {
+    float *yb = p.y + (int64_t)ch * p.y_stride + (p.start - p.y_lo);
+    const __amdgpu_buffer_rsrc_t ys =
+        __builtin_amdgcn_make_buffer_rsrc(yb, (short)0, (int)((p.end - p.start) * 4), 0x00020000);
+    const int cmin = p.half, cmax = kFft32L - p.half;
+    const int64_t off = n0 - cmin - p.start;
+    const int64_t oend = p.end - p.start;
+    float pk = 0.0f;
+    auto F = [&](int n, float &f0, float &f1) {
+        const int s = (n & 1) ? sg : 0;
+        f0 = __int_as_float(__float_as_int((float)o[n].x) ^ s);
+        f1 = __int_as_float(__float_as_int((float)(-o[n].y)) ^ s);
+    };
+    if ((cmin & 3) == 0 && n0 >= p.start && n0 + B <= p.end) {
+        // quad stores: lanes j and j ^ 1 trade one pair (DPP quad_perm [1,0,3,2])
+        const bool odd = j & 1;
+        const int jq = j & ~1;
+        using b128_t = decltype(__builtin_amdgcn_raw_buffer_load_b128(ys, 0, 0, 0));
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            float a0, a1, b0, b1;
+            F(2 * k, a0, a1);
+            F(2 * k + 1, b0, b1);
+            const int ca = 2 * (j + 1024 * k), cb = ca + 1024;
+            const bool oka = ca >= cmin && ca < cmax, okb = cb >= cmin && cb < cmax;
+            pk = fmaxf(pk, fmaxf(oka ? fmaxf(fabsf(a0), fabsf(a1)) : 0.0f, okb ? fmaxf(fabsf(b0), fabsf(b1)) : 0.0f));
+            const int s0 = __float_as_int(odd ? a0 : b0), s1 = __float_as_int(odd ? a1 : b1);
+            const int r0 = __builtin_amdgcn_update_dpp(0, s0, 0xB1, 0xF, 0xF, false);
+            const int r1 = __builtin_amdgcn_update_dpp(0, s1, 0xB1, 0xF, 0xF, false);
+            int4 q;
+            q.x = odd ? r0 : __float_as_int(a0);
+            q.y = odd ? r1 : __float_as_int(a1);
+            q.z = odd ? __float_as_int(b0) : r0;
+            q.w = odd ? __float_as_int(b1) : r1;
+            const int cq = 2 * (jq + 512 * (2 * k + (odd ? 1 : 0)));
+            const bool okq = cq >= cmin && cq < cmax;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(b128_t, q), ys,
+                                                   okq ? (int)((off + cq) * 4) : (int)0x80000000, 0, kFft32StoreAux);
+        }
+    } else {
+#pragma unroll
+        for (int n = 0; n < 32; ++n) {
+            const int c = 2 * (j + 512 * n);
+            float f0, f1;
+            F(n, f0, f1);
+            const int64_t oo = off + c;
+            const bool ok0 = c >= cmin && c < cmax && oo >= 0 && oo < oend,
+                       ok1 = c + 1 >= cmin && c + 1 < cmax && oo + 1 >= 0 && oo + 1 < oend;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(f0), ys, ok0 ? (int)(oo * 4) : (int)0x80000000, 0,
+                                                  kFft32StoreAux);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(f1), ys, ok1 ? (int)(oo * 4 + 4) : (int)0x80000000,
+                                                  0, kFft32StoreAux);
+            pk = fmaxf(pk, fmaxf(ok0 ? fabsf(f0) : 0.0f, ok1 ? fabsf(f1) : 0.0f));
+        }
+    }
+    return pk;
+}
+
+// Persistent, XCD-aware grid as fir_fft_f64_kernel (one 512-thread workgroup
+// per CU, fft_unit32), zero-phase single-partition filters (kFftOutSym).
+// pair: kR32PairTable (fft_plan_tables); tw: kR32Tw twiddles; task: 512
+// r32_task_word; c8: the special lane's bin-N/2 coefficient (real).
+template <int kOut = kFftOutSym> // a template, so host-only users of this header emit no kernel stub
+__global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, const double2 *__restrict__ pair,
+                                                           const double2 *__restrict__ tw,
+                                                           const uint32_t *__restrict__ task, int B, FftGrid gd,
+                                                           double c8) {
+    extern __shared__ double2 flds[];
+    double2 *twl = flds + kFftM; // kR32Tw twiddles, then 8 f32 peak slots, then the special lane's scratch
+    for (int i = threadIdx.x; i < kR32Tw; i += kFftNT) twl[i] = tw[i];
+    float *pk_lds = reinterpret_cast<float *>(twl + kR32Tw);
+    double2 *spl = twl + kR32Tw + 2;
+    {
+        const int u = fft_unit32(0, blockIdx.x, gridDim.x, gd.units);
+        const int c = fft_div(u, gd);
+        r32_stage_samples(p, c, p.seg0 + (int64_t)(u - c * gd.nseg) * B, threadIdx.x, flds);
+    }
+    __builtin_amdgcn_s_waitcnt(kVmcnt0);
+    __syncthreads();
+    uint32_t tk_all = task[threadIdx.x];
+    asm volatile("" : "+v"(tk_all));
+    float pk_run = 0.0f;
+    int pk_ch = -1;
+    int pk_pending = -1;
+    int rnd = 0;
+    for (int u = fft_unit32(0, blockIdx.x, gridDim.x, gd.units); u < gd.units;
+         u = fft_unit32(++rnd, blockIdx.x, gridDim.x, gd.units)) {
+        int j = threadIdx.x;
+        asm volatile("" : "+v"(j));
+        const int w = j >> 6, lane = j & 63;
+        const int wu = __builtin_amdgcn_readfirstlane(w);
+        const bool hi = wu >= 4; // waves 4..7: rotated stage-1 / final DFT32s
+        const int ch = fft_div(u, gd);
+        const int64_t n0 = p.seg0 + (int64_t)(u - ch * gd.nseg) * B;
+        double2 a[32];
+        // ---- stage 1: the samples out of the wave's region (staged by the
+        // previous unit), waves 4..7 negating the odd ones; DFT32; W_16384^(b k1)
+        {
+            const float2 *fz = reinterpret_cast<const float2 *>(flds) + 2048 * w + lane;
+            const int sg = hi ? (int)0x80000000 : 0;
+#pragma unroll
+            for (int n = 0; n < 32; ++n) {
+                float2 v = fz[64 * n];
+                if (n & 1) {
+                    v.x = __int_as_float(__float_as_int(v.x) ^ sg);
+                    v.y = __int_as_float(__float_as_int(v.y) ^ sg);
+                }
+                a[n] = make_double2((double)v.x, (double)v.y);
+            }
+        }
+        dft32(a);
+        {
+            // register r holds k1 = r + 16 hi (mod 32): powers w^(16 hi) w^r, w^(16 (1 - hi)) w^(r - 16)
+            const double2 wb = twl[kR32TwB + j], w16 = twl[kR32TwB16 + j], one = make_double2(1.0, 0.0);
+            r32_chain16(a, 0, csel(hi, w16, one), wb);
+            r32_chain16(a, 16, csel(hi, one, w16), wb);
+        }
+        // ---- T1 round 1: registers 0..15 into the wave's own region (its lanes
+        // read their samples from it above: issue order is enough)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) flds[1024 * w + 64 * i + lane] = a[i];
+        __syncthreads();
+        if (pk_pending >= 0) {
+            if (threadIdx.x == 0) fft_peak_commit(p, pk_pending, pk_lds);
+            pk_pending = -1;
+        }
+        const int g = lane >> 5, h = (lane >> 4) & 1, gam = lane & 15;
+        const int k1 = r32_column(w, g, h);
+        double2 c[32];
+        {
+            // from thread b = 16 (i + 16 h) + gam, its register k1 & 15
+            const int base = 4096 * h + 64 * (k1 & 15) + gam;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) c[i] = flds[base + 1024 * (i >> 2) + 16 * (i & 3)];
+        }
+        __syncthreads();
+        // ---- T1 round 2: registers 16..31 (k1 = 16 + i, or i for waves 4..7)
+        // into the region of their column's wave
+        {
+            const int base = 16 * ((j >> 4) & 15) + (j & 15);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int home = hi ? r32_column_home(i) : r32_column_home(16 + i); // uniform
+                flds[1024 * (home >> 2) + 256 * (home & 3) + base] = a[16 + i];
+            }
+        }
+        __syncthreads();
+        {
+            const int base = 1024 * w + 256 * (2 * g + h) + gam;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) c[16 + i] = flds[base + 16 * i];
+        }
+        // ---- stage 2: DFT32 over beta (rotated by 16 h), * (s W_512^gam)^kappa, s = (-1)^h
+        dft32(c);
+        double2 wg = twl[kR32TwG + gam];
+        if (h) wg = make_double2(-wg.x, -wg.y);
+        r32_chain32(c, wg);
+        // ---- the pair table's first half, in flight across T2
+        double2 pq[16], p2v[8];
+        {
+            const double2 *pt = pair + j;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) pq[i] = pt[512 * i];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) p2v[m] = pt[512 * (16 + m)];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- T2: two wave-local rounds (kappa < 16, kappa >= 16) in the wave's region
+        uint32_t tk = tk_all;
+        asm volatile("" : "+v"(tk)); // per unit: T2's addresses are not hoisted out of the loop
+        const int x1 = (tk >> 1) & 15, x2 = (tk >> 6) & 15;
+        const int rb1 = 1024 * w + 512 * g + 256 * (tk & 1) + 16 * x1;
+        const int rb2 = 1024 * w + 512 * g + 256 * ((tk >> 5) & 1) + 16 * x2;
+        const int wb2 = 1024 * w + 512 * g + 256 * h;
+        double2 R1[16], R2[16];
+#pragma unroll
+        for (int kl = 0; kl < 16; ++kl) flds[wb2 + 16 * kl + (gam ^ kl)] = c[kl];
+        wave_lds_sync();
+#pragma unroll
+        for (int i = 0; i < 16; ++i) R1[i] = flds[rb1 + (i ^ x1)];
+        wave_lds_sync();
+#pragma unroll
+        for (int kl = 0; kl < 16; ++kl) flds[wb2 + 16 * kl + (gam ^ kl)] = c[16 + kl];
+        wave_lds_sync();
+#pragma unroll
+        for (int i = 0; i < 16; ++i) R2[i] = flds[rb2 + (i ^ x2)];
+        // ---- stage 3: DFT16 over gamma -> lambda
+        dft16(R1);
+        dft16(R2);
+        // ---- pair step: slot i pairs R1[i] (bin k) with R2[15 - i] (bin N - k);
+        // the special lane permutes its registers into that layout first
+        const bool sp = wu == 0 && lane == kR32SpecialLane;
+        double2 v8 = R1[8];
+        if (R32_SPECIAL && wu == 0) {
+            if (sp) {
+                // x' = [R2 0..7, R1 1..7, R1 0], y' = [R1 0, R1 9..15, R2 8..15]; R1[8] (bin N/2) apart
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    spl[i] = R1[i];
+                    spl[16 + i] = R2[i];
+                }
+#pragma unroll
+                for (int i = 0; i < 8; ++i) R1[i] = spl[16 + i];
+#pragma unroll
+                for (int i = 8; i < 15; ++i) R1[i] = spl[i - 7];
+                R1[15] = spl[0];
+                R2[0] = spl[0];
+#pragma unroll
+                for (int i = 1; i < 8; ++i) R2[i] = spl[8 + i];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            fft_pair_sym(R1[i], R2[15 - i], pq[i].x, pq[i].y, (i & 1) ? p2v[i >> 1].y : p2v[i >> 1].x, R1[i],
+                         R2[15 - i]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        {
+            // the second half of the table (its registers were the first half's)
+            const double2 *pt = pair + j;
+#pragma unroll
+            for (int i = 8; i < 16; ++i) pq[i] = pt[512 * i];
+#pragma unroll
+            for (int m = 4; m < 8; ++m) p2v[m] = pt[512 * (16 + m)];
+        }
+#pragma unroll
+        for (int i = 8; i < 16; ++i) {
+            fft_pair_sym(R1[i], R2[15 - i], pq[i].x, pq[i].y, (i & 1) ? p2v[i >> 1].y : p2v[i >> 1].x, R1[i],
+                         R2[15 - i]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (R32_SPECIAL && wu == 0) {
+            if (sp) {
+                // back: R1 = [x 15, x 8..14, conj(c8 v8), y 1..7], R2 = [x 0..7, y 8..15]
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    spl[i] = R1[i];
+                    spl[16 + i] = R2[i];
+                }
+                R1[0] = spl[15];
+#pragma unroll
+                for (int i = 1; i < 8; ++i) R1[i] = spl[7 + i];
+                R1[8] = make_double2(v8.x * c8, -v8.y * c8);
+#pragma unroll
+                for (int i = 9; i < 16; ++i) R1[i] = spl[16 + i - 8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) R2[i] = spl[i];
+            }
+        }
+        // ---- inverse stage 3: DFT16 over lambda -> gamma (on conj(V))
+        dft16(R1);
+        dft16(R2);
+        // ---- T2 backwards (addresses recomputed from laundered words: the 32
+        // of T2 would otherwise stay live across the pair step)
+        {
+            uint32_t tkb = tk_all;
+            int jb = threadIdx.x;
+            asm volatile("" : "+v"(tkb), "+v"(jb));
+            const int wb_ = jb >> 6, gb_ = (jb >> 5) & 1, hb_ = (jb >> 4) & 1, gmb = jb & 15;
+            const int y1 = (tkb >> 1) & 15, y2 = (tkb >> 6) & 15;
+            const int sb1 = 1024 * wb_ + 512 * gb_ + 256 * (tkb & 1) + 16 * y1;
+            const int sb2 = 1024 * wb_ + 512 * gb_ + 256 * ((tkb >> 5) & 1) + 16 * y2;
+            const int sbw = 1024 * wb_ + 512 * gb_ + 256 * hb_;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) flds[sb1 + (i ^ y1)] = R1[i];
+            wave_lds_sync();
+#pragma unroll
+            for (int kl = 0; kl < 16; ++kl) c[kl] = flds[sbw + 16 * kl + (gmb ^ kl)];
+            wave_lds_sync();
+#pragma unroll
+            for (int i = 0; i < 16; ++i) flds[sb2 + (i ^ y2)] = R2[i];
+            wave_lds_sync();
+#pragma unroll
+            for (int kl = 0; kl < 16; ++kl) c[16 + kl] = flds[sbw + 16 * kl + (gmb ^ kl)];
+        }
+        // ---- inverse stage 2: * (s W_512^gam)^kappa, DFT32 (outputs rotated by 16 h).
+        // The powers are rebuilt, not kept from stage 2 (124 VGPRs across the
+        // pair step): the laundered base stops the compiler from reusing them.
+        asm volatile("" : "+v"(wg.x), "+v"(wg.y));
+        r32_chain32(c, wg);
+        dft32(c);
+        wave_lds_sync();
+        // ---- T1 backwards, round 1: registers 0..15 into the wave's own region
+#pragma unroll
+        for (int i = 0; i < 16; ++i) flds[1024 * w + 64 * i + lane] = c[i];
+        __syncthreads();
+        {
+            // thread b: register r holds k1 = r + 16 hi, from lane (k1, gamma_b)'s register beta_b & 15
+            const int base = 64 * ((j >> 4) & 15) + (j & 15);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int home = hi ? r32_column_home(16 + r) : r32_column_home(r); // uniform
+                a[r] = flds[1024 * (home >> 2) + 16 * (home & 3) + base];
+            }
+        }
+        __syncthreads();
+        {
+            // registers 16..31: beta = i + 16 (1 - h) -> thread 16 beta + gam's region
+            const int base = 4096 * (1 - h) + 64 * (k1 & 15) + gam;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) flds[base + 1024 * (i >> 2) + 16 * (i & 3)] = c[16 + i];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 16; ++i) a[16 + i] = flds[1024 * w + 64 * i + lane];
+        // vmcnt(0) lgkmcnt(0): the wave's reads of its region have retired (and
+        // the compiler's vmcnt accounting ignores LDS-DMA; see fir_fft32.hpp)
+        __builtin_amdgcn_s_waitcnt(0x0070);
+        {
+            const int un1 = fft_unit32(rnd + 1, blockIdx.x, gridDim.x, gd.units);
+            const int un = un1 < gd.units ? un1 : u;
+            const int cn = fft_div(un, gd);
+            r32_stage_samples(p, cn, p.seg0 + (int64_t)(un - cn * gd.nseg) * B, j, flds);
+        }
+        // ---- final: * W_16384^(b k1), DFT32 over k1 -> n
+        {
+            const double2 wb = twl[kR32TwB + j], w16 = twl[kR32TwB16 + j], one = make_double2(1.0, 0.0);
+            r32_chain16(a, 0, csel(hi, w16, one), wb);
+            r32_chain16(a, 16, csel(hi, one, w16), wb);
+        }
+        dft32(a);
+        __builtin_amdgcn_s_waitcnt(kVmcnt0); // the staging transfers have landed (stage 1 reads them)
+        const float pk = r32_store_unit(p, ch, n0, B, j, a, hi ? (int)0x80000000 : 0);
+        if (ch != pk_ch) {
+            if (p.peak && pk_ch >= 0) {
+                fft_peak_stage(pk_lds, pk_run);
+                pk_pending = pk_ch;
+                asm volatile("" : "+v"(pk_pending));
+            }
+            pk_run = 0.0f;
+            pk_ch = ch;
+        }
+        pk_run = fmaxf(pk_run, pk);
+    }
+    __builtin_amdgcn_s_waitcnt(kVmcnt0);
+    if (p.peak && pk_ch >= 0) {
+        __syncthreads();
+        if (pk_pending >= 0 && threadIdx.x == 0) fft_peak_commit(p, pk_pending, pk_lds);
+        __syncthreads();
+        fft_peak_stage(pk_lds, pk_run);
+        __syncthreads();
+        if (threadIdx.x == 0) fft_peak_commit(p, pk_ch, pk_lds);
+    }
+}
