@@ -37,7 +37,7 @@
 //     outputs, folded into the f32 stores' sign bits.
 // Wave 0's lane 31 holds the self-paired bins 0 and N/2 (tasks (0, 0) and
 // (0, 16)); it permutes its registers through a 512-B LDS scratch before and
-// after the pair step.  scripts/fft32r_model.py is the numpy model of this
+// after the pair step (per-lane select chains in place spilled VGPRs).  scripts/fft32r_model.py is the numpy model of this
 // flow (every register index, LDS slot and table slot; bank conflicts).
 //
 // Included by fir_fft.hpp after fir_fft32.hpp, inside namespace lcfir.
@@ -48,8 +48,27 @@ constexpr int kR32TwG = 1024;   // W_512^g, g < 16
 constexpr int kR32Tw = 1024 + 16;
 constexpr size_t kR32PairTable = (size_t)24 * kFftNT; // double2: (p1, q2) [16][512], (p2 even, p2 odd) [8][512]
 constexpr int kR32SpecialLane = 31;                   // of wave 0
-#ifndef R32_SPECIAL
-#define R32_SPECIAL 1
+#ifndef LCFIR_R32_REGLOAD
+#define LCFIR_R32_REGLOAD 0 // 1: the next unit's samples by register loads issued in T1 backwards (no LDS-DMA)
+#endif
+#ifndef LCFIR_R32_PRIO
+#define LCFIR_R32_PRIO 0 // tools builds: issue priority of waves 4..7 (1 always, 2 BAR6..BAR1, 3 BAR3..BAR4)
+#endif
+
+// Phase timestamps for tools/fft32r_trace.hip (off in the product build):
+// lane 0 of every wave of workgroups < 64 records s_memtime at each phase
+// boundary of its 3rd unit.
+#ifdef LCFIR_FFT32R_TRACE
+__device__ unsigned long long g_fft32r_trace[64][8][24];
+#define R32_STAMP(i)                                                                        \
+    do {                                                                                    \
+        if (blockIdx.x < 64 && rnd == 2 && (threadIdx.x & 63) == 0)                         \
+            g_fft32r_trace[blockIdx.x][threadIdx.x >> 6][i] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define R32_STAMP(i) \
+    do {             \
+    } while (0)
 #endif
 
 // column k1 of lane (wave w, 32-lane group g, half h); mirror columns k1 and
@@ -277,15 +296,20 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
     for (int i = threadIdx.x; i < kR32Tw; i += kFftNT) twl[i] = tw[i];
     float *pk_lds = reinterpret_cast<float *>(twl + kR32Tw);
     double2 *spl = twl + kR32Tw + 2;
+    float2 v[32]; // LCFIR_R32_REGLOAD: the samples of the unit about to start
     {
         const int u = fft_unit32(0, blockIdx.x, gridDim.x, gd.units);
         const int c = fft_div(u, gd);
-        r32_stage_samples(p, c, p.seg0 + (int64_t)(u - c * gd.nseg) * B, threadIdx.x, flds);
+        if (LCFIR_R32_REGLOAD)
+            fft_load_unit<32>(p, c, p.seg0 + (int64_t)(u - c * gd.nseg) * B, threadIdx.x, v);
+        else
+            r32_stage_samples(p, c, p.seg0 + (int64_t)(u - c * gd.nseg) * B, threadIdx.x, flds);
     }
     __builtin_amdgcn_s_waitcnt(kVmcnt0);
     __syncthreads();
     uint32_t tk_all = task[threadIdx.x];
     asm volatile("" : "+v"(tk_all));
+    if (LCFIR_R32_PRIO == 1 && __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= 4) __builtin_amdgcn_s_setprio(1);
     float pk_run = 0.0f;
     int pk_ch = -1;
     int pk_pending = -1;
@@ -300,6 +324,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
         const int ch = fft_div(u, gd);
         const int64_t n0 = p.seg0 + (int64_t)(u - ch * gd.nseg) * B;
         double2 a[32];
+        R32_STAMP(0);
         // ---- stage 1: the samples out of the wave's region (staged by the
         // previous unit), waves 4..7 negating the odd ones; DFT32; W_16384^(b k1)
         {
@@ -307,12 +332,12 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
             const int sg = hi ? (int)0x80000000 : 0;
 #pragma unroll
             for (int n = 0; n < 32; ++n) {
-                float2 v = fz[64 * n];
+                float2 vn = LCFIR_R32_REGLOAD ? v[n] : fz[64 * n];
                 if (n & 1) {
-                    v.x = __int_as_float(__float_as_int(v.x) ^ sg);
-                    v.y = __int_as_float(__float_as_int(v.y) ^ sg);
+                    vn.x = __int_as_float(__float_as_int(vn.x) ^ sg);
+                    vn.y = __int_as_float(__float_as_int(vn.y) ^ sg);
                 }
-                a[n] = make_double2((double)v.x, (double)v.y);
+                a[n] = make_double2((double)vn.x, (double)vn.y);
             }
         }
         dft32(a);
@@ -322,11 +347,15 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
             r32_chain16(a, 0, csel(hi, w16, one), wb);
             r32_chain16(a, 16, csel(hi, one, w16), wb);
         }
+        R32_STAMP(1);
         // ---- T1 round 1: registers 0..15 into the wave's own region (its lanes
         // read their samples from it above: issue order is enough)
 #pragma unroll
         for (int i = 0; i < 16; ++i) flds[1024 * w + 64 * i + lane] = a[i];
+        R32_STAMP(2);
         __syncthreads();
+        R32_STAMP(3);
+        if (LCFIR_R32_PRIO == 2 && hi) __builtin_amdgcn_s_setprio(0);
         if (pk_pending >= 0) {
             if (threadIdx.x == 0) fft_peak_commit(p, pk_pending, pk_lds);
             pk_pending = -1;
@@ -340,7 +369,9 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
 #pragma unroll
             for (int i = 0; i < 16; ++i) c[i] = flds[base + 1024 * (i >> 2) + 16 * (i & 3)];
         }
+        R32_STAMP(4);
         __syncthreads();
+        R32_STAMP(5);
         // ---- T1 round 2: registers 16..31 (k1 = 16 + i, or i for waves 4..7)
         // into the region of their column's wave
         {
@@ -351,17 +382,21 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
                 flds[1024 * (home >> 2) + 256 * (home & 3) + base] = a[16 + i];
             }
         }
+        R32_STAMP(6);
         __syncthreads();
+        if (LCFIR_R32_PRIO == 3 && hi) __builtin_amdgcn_s_setprio(1);
         {
             const int base = 1024 * w + 256 * (2 * g + h) + gam;
 #pragma unroll
             for (int i = 0; i < 16; ++i) c[16 + i] = flds[base + 16 * i];
         }
+        R32_STAMP(7);
         // ---- stage 2: DFT32 over beta (rotated by 16 h), * (s W_512^gam)^kappa, s = (-1)^h
         dft32(c);
         double2 wg = twl[kR32TwG + gam];
         if (h) wg = make_double2(-wg.x, -wg.y);
         r32_chain32(c, wg);
+        R32_STAMP(8);
         // ---- the pair table's first half, in flight across T2
         double2 pq[16], p2v[8];
         {
@@ -372,6 +407,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
             for (int m = 0; m < 4; ++m) p2v[m] = pt[512 * (16 + m)];
         }
         __builtin_amdgcn_sched_barrier(0);
+        R32_STAMP(9);
         // ---- T2: two wave-local rounds (kappa < 16, kappa >= 16) in the wave's region
         uint32_t tk = tk_all;
         asm volatile("" : "+v"(tk)); // per unit: T2's addresses are not hoisted out of the loop
@@ -391,14 +427,16 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
         wave_lds_sync();
 #pragma unroll
         for (int i = 0; i < 16; ++i) R2[i] = flds[rb2 + (i ^ x2)];
+        R32_STAMP(10);
         // ---- stage 3: DFT16 over gamma -> lambda
         dft16(R1);
         dft16(R2);
+        R32_STAMP(11);
         // ---- pair step: slot i pairs R1[i] (bin k) with R2[15 - i] (bin N - k);
         // the special lane permutes its registers into that layout first
         const bool sp = wu == 0 && lane == kR32SpecialLane;
         double2 v8 = R1[8];
-        if (R32_SPECIAL && wu == 0) {
+        if (wu == 0) {
             if (sp) {
                 // x' = [R2 0..7, R1 1..7, R1 0], y' = [R1 0, R1 9..15, R2 8..15]; R1[8] (bin N/2) apart
 #pragma unroll
@@ -436,7 +474,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
                          R2[15 - i]);
             __builtin_amdgcn_sched_barrier(0);
         }
-        if (R32_SPECIAL && wu == 0) {
+        if (wu == 0) {
             if (sp) {
                 // back: R1 = [x 15, x 8..14, conj(c8 v8), y 1..7], R2 = [x 0..7, y 8..15]
 #pragma unroll
@@ -457,6 +495,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
         // ---- inverse stage 3: DFT16 over lambda -> gamma (on conj(V))
         dft16(R1);
         dft16(R2);
+        R32_STAMP(13);
         // ---- T2 backwards (addresses recomputed from laundered words: the 32
         // of T2 would otherwise stay live across the pair step)
         {
@@ -480,6 +519,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
 #pragma unroll
             for (int kl = 0; kl < 16; ++kl) c[16 + kl] = flds[sbw + 16 * kl + (gmb ^ kl)];
         }
+        R32_STAMP(14);
         // ---- inverse stage 2: * (s W_512^gam)^kappa, DFT32 (outputs rotated by 16 h).
         // The powers are rebuilt, not kept from stage 2 (124 VGPRs across the
         // pair step): the laundered base stops the compiler from reusing them.
@@ -487,10 +527,14 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
         r32_chain32(c, wg);
         dft32(c);
         wave_lds_sync();
+        R32_STAMP(15);
         // ---- T1 backwards, round 1: registers 0..15 into the wave's own region
 #pragma unroll
         for (int i = 0; i < 16; ++i) flds[1024 * w + 64 * i + lane] = c[i];
+        R32_STAMP(16);
         __syncthreads();
+        R32_STAMP(17);
+        if (LCFIR_R32_PRIO == 3 && hi) __builtin_amdgcn_s_setprio(0);
         {
             // thread b: register r holds k1 = r + 16 hi, from lane (k1, gamma_b)'s register beta_b & 15
             const int base = 64 * ((j >> 4) & 15) + (j & 15);
@@ -500,25 +544,39 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
                 a[r] = flds[1024 * (home >> 2) + 16 * (home & 3) + base];
             }
         }
+        R32_STAMP(18);
         __syncthreads();
+        R32_STAMP(19);
         {
             // registers 16..31: beta = i + 16 (1 - h) -> thread 16 beta + gam's region
             const int base = 4096 * (1 - h) + 64 * (k1 & 15) + gam;
 #pragma unroll
             for (int i = 0; i < 16; ++i) flds[base + 1024 * (i >> 2) + 16 * (i & 3)] = c[16 + i];
         }
+        if (LCFIR_R32_REGLOAD) {
+            // the next unit's samples, in flight across the last barrier and
+            // the final DFT (the last unit reloads itself)
+            const int un1 = fft_unit32(rnd + 1, blockIdx.x, gridDim.x, gd.units);
+            const int un = un1 < gd.units ? un1 : u;
+            const int cn = fft_div(un, gd);
+            fft_load_unit<32>(p, cn, p.seg0 + (int64_t)(un - cn * gd.nseg) * B, j, v);
+        }
+        R32_STAMP(20);
         __syncthreads();
+        if (LCFIR_R32_PRIO == 2 && hi) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < 16; ++i) a[16 + i] = flds[1024 * w + 64 * i + lane];
+        R32_STAMP(21);
         // vmcnt(0) lgkmcnt(0): the wave's reads of its region have retired (and
         // the compiler's vmcnt accounting ignores LDS-DMA; see fir_fft32.hpp)
-        __builtin_amdgcn_s_waitcnt(0x0070);
-        {
+        if (!LCFIR_R32_REGLOAD) {
+            __builtin_amdgcn_s_waitcnt(0x0070);
             const int un1 = fft_unit32(rnd + 1, blockIdx.x, gridDim.x, gd.units);
             const int un = un1 < gd.units ? un1 : u;
             const int cn = fft_div(un, gd);
             r32_stage_samples(p, cn, p.seg0 + (int64_t)(un - cn * gd.nseg) * B, j, flds);
         }
+        R32_STAMP(22);
         // ---- final: * W_16384^(b k1), DFT32 over k1 -> n
         {
             const double2 wb = twl[kR32TwB + j], w16 = twl[kR32TwB16 + j], one = make_double2(1.0, 0.0);
@@ -538,6 +596,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
             pk_ch = ch;
         }
         pk_run = fmaxf(pk_run, pk);
+        R32_STAMP(23);
     }
     __builtin_amdgcn_s_waitcnt(kVmcnt0);
     if (p.peak && pk_ch >= 0) {

@@ -1,0 +1,152 @@
+// fft32r_trace.hip -- phase timeline of fir_fft32r_kernel (development tool,
+// not part of the product): fft32_trace.hip for the register-resident
+// L = 32 768 kernel.  Runs a config-3 shaped launch (8 x 5.76 M samples,
+// 8001 symmetric taps) and prints, per wave, the average shader cycles of each
+// phase of a steady-state unit over 64 workgroups.
+//   hipcc -O3 -std=c++2b --offload-arch=gfx950 -I../csrc -DLCFIR_FFT32R=1 -DLCFIR_FFT32R_TRACE \
+//         fft32r_trace.hip -o fft32r_trace
+//   ./fft32r_trace [ntaps] [seg_len]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "fir_fft.hpp"
+
+#define CK(x)                                                                   \
+    do {                                                                        \
+        hipError_t e_ = (x);                                                    \
+        if (e_ != hipSuccess) {                                                 \
+            std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));        \
+            std::exit(1);                                                       \
+        }                                                                       \
+    } while (0)
+
+static const char *kNames[] = {"stage1 (samples, dft32, tw)", "T1 w1", "BAR1", "peak + T1 r1", "BAR2",
+                               "T1 w2", "BAR3 + T1 r2", "stage2 (dft32, tw)", "pair loads A", "T2",
+                               "stage3 dft16", "pair step", "inv stage3", "T2 back", "inv stage2",
+                               "T1' w1", "BAR4", "T1' r1", "BAR5", "T1' w2", "BAR6 + T1' r2",
+                               "wait + DMA issue", "final + stores + peak"};
+constexpr int kPhases = 23;
+
+int main(int argc, char **argv) {
+    const int T = argc > 1 ? std::atoi(argv[1]) : 8001;
+    const int seg = argc > 2 ? std::atoi(argv[2]) : 32768;
+    const int64_t n = 5760000;
+    const int nch = 8;
+    std::vector<float> hx((size_t)n * nch);
+    uint64_t s = 12345;
+    for (auto &v : hx) {
+        s = s * 6364136223846793005ULL + 1442695040888963407ULL;
+        v = (float)((double)(s >> 11) / 9007199254740992.0 - 0.5);
+    }
+    // a symmetric low-cut (Blackman windowed sinc, spectral inversion)
+    std::vector<double> taps(T);
+    const int M = T - 1, half = M / 2;
+    double sum = 0;
+    for (int i = 0; i < T; ++i) {
+        const double d = i - half, fc = 20.0 / 96000.0;
+        const double h = d == 0 ? 2 * M_PI * fc : std::sin(2 * M_PI * fc * d) / d;
+        const double w = 0.42 - 0.5 * std::cos(2 * M_PI * i / M) + 0.08 * std::cos(4 * M_PI * i / M);
+        taps[i] = h * w;
+        sum += taps[i];
+    }
+    for (int i = 0; i < T; ++i) taps[i] = -taps[i] / sum;
+    taps[half] += 1.0;
+    for (int i = 0; i < half; ++i) taps[T - 1 - i] = taps[i];
+    if (argc > 3 && std::string(argv[3]) == "asym")
+        for (int i = 0; i < T; ++i) taps[i] += 1e-9 * (2.0 * i / M - 1.0);
+    float *dx, *dy;
+    double *dt;
+    CK(hipMalloc(&dx, sizeof(float) * hx.size()));
+    CK(hipMalloc(&dy, sizeof(float) * hx.size()));
+    CK(hipMalloc(&dt, sizeof(double) * T));
+    CK(hipMemcpy(dx, hx.data(), sizeof(float) * hx.size(), hipMemcpyHostToDevice));
+    CK(hipMemcpy(dt, taps.data(), sizeof(double) * T, hipMemcpyHostToDevice));
+    lcfir::FftPlan plan;
+    lcfir::FftTuning tune;
+    tune.seg_len = seg;
+    std::string err;
+    if (!lcfir::fft_plan_build(plan, dt, T, tune, nullptr, err)) {
+        std::fprintf(stderr, "plan: %s\n", err.c_str());
+        return 1;
+    }
+    std::printf("plan: L %d, parts %d, zero-phase %d, B %d\n", plan.L, plan.parts, (int)plan.sym, plan.B);
+    lcfir::DirectParams p{};
+    p.x = dx;
+    p.x_lo = 0;
+    p.x_hi = n;
+    p.x_stride = n;
+    p.y = dy;
+    p.y_lo = 0;
+    p.y_stride = n;
+    p.taps = dt;
+    p.ntaps = T;
+    p.half = half;
+    p.start = 0;
+    p.end = n;
+    unsigned *dpeak = nullptr;
+    CK(hipMalloc(&dpeak, 64));
+    CK(hipMemset(dpeak, 0, 64));
+    p.peak = dpeak;
+    p.peak_stride = 1;
+    const size_t npark = lcfir::fft32_park_doubles(plan);
+    if (npark) CK(hipMalloc(reinterpret_cast<void **>(&p.park), npark * sizeof(double)));
+    const size_t nscr = lcfir::fft_scratch_doubles(plan, p, nch);
+    if (nscr) {
+        CK(hipMalloc(reinterpret_cast<void **>(&p.y64), nscr * sizeof(double)));
+        p.y64_stride = std::min<int64_t>(p.end - p.start, lcfir::fft_chunk_span(plan));
+    }
+    auto launch = [&]() { return lcfir::fft_launch(plan, p, nch, nullptr, err); };
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int it = 0; it < 20; ++it)
+        if (!launch()) return 1;
+    const int reps = 10, rounds = 5;
+    std::vector<float> per;
+    for (int r = 0; r < rounds; ++r) {
+        CK(hipEventRecord(e0));
+        for (int it = 0; it < reps; ++it)
+            if (!launch()) return 1;
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float t = 0;
+        CK(hipEventElapsedTime(&t, e0, e1));
+        per.push_back(t);
+    }
+    std::sort(per.begin(), per.end());
+    const float ms = per[rounds / 2], ms_min = per[0];
+    const int64_t units = (int64_t)((n + plan.B - 1) / plan.B) * nch;
+    std::printf("kernel %.4f ms (min %.4f)  (%.1f Gsamples/s), units %lld, units/WG %.2f\n", ms / reps, ms_min / reps,
+                (double)n * nch / (ms / reps * 1e-3) / 1e9, (long long)units, (double)units / plan.cus);
+#ifdef LCFIR_FFT32R_TRACE
+    static unsigned long long tr[64][8][24];
+    CK(hipMemcpyFromSymbol(tr, HIP_SYMBOL(lcfir::g_fft32r_trace), sizeof(tr)));
+    std::printf("%-32s", "phase \\ wave");
+    for (int w = 0; w < 8; ++w) std::printf("%8d", w);
+    std::printf("%8s\n", "avg");
+    double total[8] = {0};
+    for (int ph = 0; ph < kPhases; ++ph) {
+        std::printf("%-32s", kNames[ph]);
+        double sum2 = 0;
+        for (int w = 0; w < 8; ++w) {
+            double acc = 0;
+            for (int g = 0; g < 64; ++g) acc += (double)(tr[g][w][ph + 1] - tr[g][w][ph]);
+            acc /= 64;
+            total[w] += acc;
+            sum2 += acc;
+            std::printf("%8.0f", acc);
+        }
+        std::printf("%8.0f\n", sum2 / 8);
+    }
+    std::printf("%-32s", "unit total");
+    for (int w = 0; w < 8; ++w) std::printf("%8.0f", total[w]);
+    std::printf("\n");
+#endif
+    return 0;
+}
