@@ -207,11 +207,16 @@ inline int fft_partition_count(int ntaps, int L = 16384) {
 // partial sums; an L = 32 768 unit is two 8192-point halves plus the split,
 // the merge and the park slab, the general pair table and partitions cost
 // more there (register pressure).
+// Zero-phase single-partition L = 32768 plans run fir_fft32r_kernel (the
+// transform held in registers) unless a tools build turns it off; its unit
+// costs 2.2 L = 16 384 units (configs 2 and 3: 23.6 us against 10.7 us per
+// persistent-grid round), so it takes linear-phase filters
+// from ~4 000 taps (config 2's 4 001: 7.65e-5 against 8.07e-5 per output).
 #ifndef LCFIR_FFT32R
-#define LCFIR_FFT32R 0 // 1: zero-phase single-partition L = 32768 plans run fir_fft32r_kernel
+#define LCFIR_FFT32R 1
 #endif
 #ifndef LCFIR_FFT32R_COST
-#define LCFIR_FFT32R_COST 2.9
+#define LCFIR_FFT32R_COST 2.2
 #endif
 inline bool fft_reg32(int L, int parts, bool sym) { return LCFIR_FFT32R && L == 32768 && parts == 1 && sym; }
 inline double fft_unit_cost(int L, int parts, bool sym) {
@@ -1609,7 +1614,7 @@ inline int64_t fft_chunk(const FftPlan &plan) {
 }
 
 // work array + twiddles + 8 f32 peak slots + the special lane's 32 double2
-constexpr size_t kR32LdsBytes = sizeof(double2) * (size_t)(kFftM + kR32Tw + 2 + 32);
+constexpr size_t kR32LdsBytes = sizeof(double2) * (size_t)(kR32Work + kR32Tw + 2 + 32);
 
 template <int kOut>
 inline bool fft32r_launch_one(const FftPlan &plan, const DirectParams &q, int nch, hipStream_t s, std::string &err) {

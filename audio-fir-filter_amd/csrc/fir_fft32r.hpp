@@ -51,6 +51,9 @@ constexpr int kR32SpecialLane = 31;                   // of wave 0
 #ifndef LCFIR_R32_REGLOAD
 #define LCFIR_R32_REGLOAD 0 // 1: the next unit's samples by register loads issued in T1 backwards (no LDS-DMA)
 #endif
+#ifndef LCFIR_R32_PAD
+#define LCFIR_R32_PAD 1 // T2's rows padded to 17 slots: conflict-free without an XOR swizzle's address math (-5 %)
+#endif
 #ifndef LCFIR_R32_PRIO
 #define LCFIR_R32_PRIO 0 // tools builds: issue priority of waves 4..7 (1 always, 2 BAR6..BAR1, 3 BAR3..BAR4)
 #endif
@@ -70,6 +73,21 @@ __device__ unsigned long long g_fft32r_trace[64][8][24];
     do {             \
     } while (0)
 #endif
+
+// LDS work array: one region per wave (T1 / T1 backwards address regions by
+// wave; T2 stays inside its wave's region), 32-lane groups and halves inside
+constexpr int kR32Rg = LCFIR_R32_PAD ? 1088 : 1024; // double2 per region
+constexpr int kR32Gs = LCFIR_R32_PAD ? 544 : 512;
+constexpr int kR32Hs = LCFIR_R32_PAD ? 272 : 256;
+constexpr int kR32Work = 8 * kR32Rg;
+// T2 slot of (half base, kappa mod 16, gamma): conflict-free for the writers
+// (8 consecutive gamma) and the readers (16 distinct kappa per read group)
+__device__ __forceinline__ int r32_t2(int base, int kl, int gam) {
+    return LCFIR_R32_PAD ? base + 17 * kl + gam : base + 16 * kl + (gam ^ kl);
+}
+// a T2 reader's slot for register i = gamma; rb = its half base + row offset
+__device__ __forceinline__ int r32_t2r(int rb, int i, int kl) { return LCFIR_R32_PAD ? rb + i : rb + (i ^ kl); }
+constexpr int kR32Row = LCFIR_R32_PAD ? 17 : 16;
 
 // column k1 of lane (wave w, 32-lane group g, half h); mirror columns k1 and
 // 32 - k1 share a group (wave 0 group 0: the self-paired columns 0 and 16)
@@ -123,7 +141,56 @@ inline void r32_task_bins(int t, int (&bx)[16], int (&by)[16]) {
     }
 }
 
-// forward 32-point DFT, natural order in and out (radix 2 x DFT16)
+// forward 16-point DFT with the W16 rotations in FMA form (fir_fft.hpp's
+// rot16_* / dft4_r2c: tan(pi/8) rotations, cos(pi/8) folded into the row's
+// radix-4): 8 f64 operations fewer than dft16
+__device__ __forceinline__ void dft16f(double2 (&a)[16]) {
+#pragma unroll
+    for (int n2 = 0; n2 < 4; ++n2) dft4(a[n2], a[4 + n2], a[8 + n2], a[12 + n2]);
+    a[10] = w16<4>(a[10]);
+    dft4(a[0], a[1], a[2], a[3]);
+    {
+        double2 o1, o3;
+        dft4_r2c(a[4], rot16_1(a[5]), rot8_1(a[6]), a[6], rot16_3(a[7]), o1, o3);
+        a[5] = o1;
+        a[7] = o3;
+    }
+    {
+        double2 o1, o3;
+        dft4_r13(a[8], rot8_1(a[9]), a[10], rot8_3(a[11]), o1, o3);
+        a[9] = o1;
+        a[11] = o3;
+    }
+    {
+        double2 o1, o3;
+        dft4_r2c(a[12], rot16_3(a[13]), rot8_3(a[14]), a[14], rot16_9(a[15]), o1, o3);
+        a[13] = o1;
+        a[15] = o3;
+    }
+    double2 t[16];
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1)
+#pragma unroll
+        for (int k2 = 0; k2 < 4; ++k2) t[k1 + 4 * k2] = a[4 * k1 + k2];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) a[i] = t[i];
+}
+
+// W32^k = cos t - i sin t (t = pi k / 16) as f (1 - i r) with |r| <= 1: f = cos t,
+// r = tan t where |cos| >= |sin|, else (-i) f (1 + i r) with f = sin t, r = cot t
+constexpr double kW32Fac[16] = {1.0, 0.98078528040323044913, 0.92387953251128675613, 0.83146961230254523708,
+                                0.70710678118654752440, 0.83146961230254523708, 0.92387953251128675613,
+                                0.98078528040323044913, 1.0, 0.98078528040323044913, 0.92387953251128675613,
+                                0.83146961230254523708, 0.70710678118654752440, 0.83146961230254523708,
+                                0.92387953251128675613, 0.98078528040323044913};
+constexpr double kW32Rat[16] = {0.0, 0.19891236737965800691, 0.41421356237309504880, 0.66817863791929891999,
+                                1.0, 0.66817863791929891999, 0.41421356237309504880, 0.19891236737965800691,
+                                0.0, -0.19891236737965800691, -0.41421356237309504880, -0.66817863791929891999,
+                                -1.0, -0.66817863791929891999, -0.41421356237309504880, -0.19891236737965800691};
+
+// forward 32-point DFT, natural order in and out: radix 2 over two DFT16s, each
+// butterfly's W32^k rotation in FMA form (the factor f folded into the
+// butterfly: 6 f64 operations per k instead of 8)
 __device__ __forceinline__ void dft32(double2 (&a)[32]) {
     double2 e[16], o[16];
 #pragma unroll
@@ -131,13 +198,25 @@ __device__ __forceinline__ void dft32(double2 (&a)[32]) {
         e[r] = a[2 * r];
         o[r] = a[2 * r + 1];
     }
-    dft16(e);
-    dft16(o);
+    dft16f(e);
+    dft16f(o);
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-        const double2 t = w32mul(o[k], k);
-        a[k] = cadd(e[k], t);
-        a[k + 16] = csub(e[k], t);
+        if (k == 0 || k == 8) {
+            const double2 t = k == 0 ? o[k] : mul_mi(o[k]);
+            a[k] = cadd(e[k], t);
+            a[k + 16] = csub(e[k], t);
+            continue;
+        }
+        const double f = kW32Fac[k], r = kW32Rat[k];
+        double2 q; // o W32^k / f
+        if (k < 5 || k > 11) // cos-major: o (1 - i r) (k >= 12: cos < 0, the sign in fs)
+            q = make_double2(__builtin_fma(r, o[k].y, o[k].x), __builtin_fma(-r, o[k].x, o[k].y));
+        else // sin-major: (-i) o (1 + i r)
+            q = make_double2(__builtin_fma(r, o[k].x, o[k].y), __builtin_fma(r, o[k].y, -o[k].x));
+        const double fs = (k >= 12) ? -f : f; // cos t < 0 on the cos-major side past pi / 2
+        a[k] = make_double2(__builtin_fma(fs, q.x, e[k].x), __builtin_fma(fs, q.y, e[k].y));
+        a[k + 16] = make_double2(__builtin_fma(-fs, q.x, e[k].x), __builtin_fma(-fs, q.y, e[k].y));
     }
 }
 
@@ -208,12 +287,12 @@ __device__ __forceinline__ void r32_stage_samples(const DirectParams &p, int ch,
         const int sofs = (int)(w0 * 4);
 #pragma unroll
         for (int s = 0; s < 16; ++s)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (fft_lds_void *)(flds + 1024 * w + 64 * s), 16, vofs,
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (fft_lds_void *)(flds + kR32Rg * w + 64 * s), 16, vofs,
                                                      sofs + 8192 * s, 0, 0);
     } else {
         float2 v[32];
         fft_load_unit<32>(p, ch, n0, j, v);
-        float2 *fz = reinterpret_cast<float2 *>(flds) + 2048 * w + lane;
+        float2 *fz = reinterpret_cast<float2 *>(flds) + 2 * kR32Rg * w + lane;
 #pragma unroll
         for (int n = 0; n < 32; ++n) fz[64 * n] = v[n];
     }
@@ -292,7 +371,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
                                                            const uint32_t *__restrict__ task, int B, FftGrid gd,
                                                            double c8) {
     extern __shared__ double2 flds[];
-    double2 *twl = flds + kFftM; // kR32Tw twiddles, then 8 f32 peak slots, then the special lane's scratch
+    double2 *twl = flds + kR32Work; // kR32Tw twiddles, then 8 f32 peak slots, then the special lane's scratch
     for (int i = threadIdx.x; i < kR32Tw; i += kFftNT) twl[i] = tw[i];
     float *pk_lds = reinterpret_cast<float *>(twl + kR32Tw);
     double2 *spl = twl + kR32Tw + 2;
@@ -328,7 +407,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
         // ---- stage 1: the samples out of the wave's region (staged by the
         // previous unit), waves 4..7 negating the odd ones; DFT32; W_16384^(b k1)
         {
-            const float2 *fz = reinterpret_cast<const float2 *>(flds) + 2048 * w + lane;
+            const float2 *fz = reinterpret_cast<const float2 *>(flds) + 2 * kR32Rg * w + lane;
             const int sg = hi ? (int)0x80000000 : 0;
 #pragma unroll
             for (int n = 0; n < 32; ++n) {
@@ -351,7 +430,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
         // ---- T1 round 1: registers 0..15 into the wave's own region (its lanes
         // read their samples from it above: issue order is enough)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) flds[1024 * w + 64 * i + lane] = a[i];
+        for (int i = 0; i < 16; ++i) flds[kR32Rg * w + 64 * i + lane] = a[i];
         R32_STAMP(2);
         __syncthreads();
         R32_STAMP(3);
@@ -365,9 +444,9 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
         double2 c[32];
         {
             // from thread b = 16 (i + 16 h) + gam, its register k1 & 15
-            const int base = 4096 * h + 64 * (k1 & 15) + gam;
+            const int base = 4 * kR32Rg * h + 64 * (k1 & 15) + gam;
 #pragma unroll
-            for (int i = 0; i < 16; ++i) c[i] = flds[base + 1024 * (i >> 2) + 16 * (i & 3)];
+            for (int i = 0; i < 16; ++i) c[i] = flds[base + kR32Rg * (i >> 2) + 16 * (i & 3)];
         }
         R32_STAMP(4);
         __syncthreads();
@@ -379,14 +458,14 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 const int home = hi ? r32_column_home(i) : r32_column_home(16 + i); // uniform
-                flds[1024 * (home >> 2) + 256 * (home & 3) + base] = a[16 + i];
+                flds[kR32Rg * (home >> 2) + 256 * (home & 3) + base] = a[16 + i];
             }
         }
         R32_STAMP(6);
         __syncthreads();
         if (LCFIR_R32_PRIO == 3 && hi) __builtin_amdgcn_s_setprio(1);
         {
-            const int base = 1024 * w + 256 * (2 * g + h) + gam;
+            const int base = kR32Rg * w + 256 * (2 * g + h) + gam;
 #pragma unroll
             for (int i = 0; i < 16; ++i) c[16 + i] = flds[base + 16 * i];
         }
@@ -412,25 +491,25 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
         uint32_t tk = tk_all;
         asm volatile("" : "+v"(tk)); // per unit: T2's addresses are not hoisted out of the loop
         const int x1 = (tk >> 1) & 15, x2 = (tk >> 6) & 15;
-        const int rb1 = 1024 * w + 512 * g + 256 * (tk & 1) + 16 * x1;
-        const int rb2 = 1024 * w + 512 * g + 256 * ((tk >> 5) & 1) + 16 * x2;
-        const int wb2 = 1024 * w + 512 * g + 256 * h;
+        const int rb1 = kR32Rg * w + kR32Gs * g + kR32Hs * (tk & 1) + kR32Row * x1;
+        const int rb2 = kR32Rg * w + kR32Gs * g + kR32Hs * ((tk >> 5) & 1) + kR32Row * x2;
+        const int wb2 = kR32Rg * w + kR32Gs * g + kR32Hs * h;
         double2 R1[16], R2[16];
 #pragma unroll
-        for (int kl = 0; kl < 16; ++kl) flds[wb2 + 16 * kl + (gam ^ kl)] = c[kl];
+        for (int kl = 0; kl < 16; ++kl) flds[r32_t2(wb2, kl, gam)] = c[kl];
         wave_lds_sync();
 #pragma unroll
-        for (int i = 0; i < 16; ++i) R1[i] = flds[rb1 + (i ^ x1)];
+        for (int i = 0; i < 16; ++i) R1[i] = flds[r32_t2r(rb1, i, x1)];
         wave_lds_sync();
 #pragma unroll
-        for (int kl = 0; kl < 16; ++kl) flds[wb2 + 16 * kl + (gam ^ kl)] = c[16 + kl];
+        for (int kl = 0; kl < 16; ++kl) flds[r32_t2(wb2, kl, gam)] = c[16 + kl];
         wave_lds_sync();
 #pragma unroll
-        for (int i = 0; i < 16; ++i) R2[i] = flds[rb2 + (i ^ x2)];
+        for (int i = 0; i < 16; ++i) R2[i] = flds[r32_t2r(rb2, i, x2)];
         R32_STAMP(10);
         // ---- stage 3: DFT16 over gamma -> lambda
-        dft16(R1);
-        dft16(R2);
+        dft16f(R1);
+        dft16f(R2);
         R32_STAMP(11);
         // ---- pair step: slot i pairs R1[i] (bin k) with R2[15 - i] (bin N - k);
         // the special lane permutes its registers into that layout first
@@ -493,8 +572,8 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
             }
         }
         // ---- inverse stage 3: DFT16 over lambda -> gamma (on conj(V))
-        dft16(R1);
-        dft16(R2);
+        dft16f(R1);
+        dft16f(R2);
         R32_STAMP(13);
         // ---- T2 backwards (addresses recomputed from laundered words: the 32
         // of T2 would otherwise stay live across the pair step)
@@ -504,20 +583,20 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
             asm volatile("" : "+v"(tkb), "+v"(jb));
             const int wb_ = jb >> 6, gb_ = (jb >> 5) & 1, hb_ = (jb >> 4) & 1, gmb = jb & 15;
             const int y1 = (tkb >> 1) & 15, y2 = (tkb >> 6) & 15;
-            const int sb1 = 1024 * wb_ + 512 * gb_ + 256 * (tkb & 1) + 16 * y1;
-            const int sb2 = 1024 * wb_ + 512 * gb_ + 256 * ((tkb >> 5) & 1) + 16 * y2;
-            const int sbw = 1024 * wb_ + 512 * gb_ + 256 * hb_;
+            const int sb1 = kR32Rg * wb_ + kR32Gs * gb_ + kR32Hs * (tkb & 1) + kR32Row * y1;
+            const int sb2 = kR32Rg * wb_ + kR32Gs * gb_ + kR32Hs * ((tkb >> 5) & 1) + kR32Row * y2;
+            const int sbw = kR32Rg * wb_ + kR32Gs * gb_ + kR32Hs * hb_;
 #pragma unroll
-            for (int i = 0; i < 16; ++i) flds[sb1 + (i ^ y1)] = R1[i];
+            for (int i = 0; i < 16; ++i) flds[r32_t2r(sb1, i, y1)] = R1[i];
             wave_lds_sync();
 #pragma unroll
-            for (int kl = 0; kl < 16; ++kl) c[kl] = flds[sbw + 16 * kl + (gmb ^ kl)];
+            for (int kl = 0; kl < 16; ++kl) c[kl] = flds[r32_t2(sbw, kl, gmb)];
             wave_lds_sync();
 #pragma unroll
-            for (int i = 0; i < 16; ++i) flds[sb2 + (i ^ y2)] = R2[i];
+            for (int i = 0; i < 16; ++i) flds[r32_t2r(sb2, i, y2)] = R2[i];
             wave_lds_sync();
 #pragma unroll
-            for (int kl = 0; kl < 16; ++kl) c[16 + kl] = flds[sbw + 16 * kl + (gmb ^ kl)];
+            for (int kl = 0; kl < 16; ++kl) c[16 + kl] = flds[r32_t2(sbw, kl, gmb)];
         }
         R32_STAMP(14);
         // ---- inverse stage 2: * (s W_512^gam)^kappa, DFT32 (outputs rotated by 16 h).
@@ -530,7 +609,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
         R32_STAMP(15);
         // ---- T1 backwards, round 1: registers 0..15 into the wave's own region
 #pragma unroll
-        for (int i = 0; i < 16; ++i) flds[1024 * w + 64 * i + lane] = c[i];
+        for (int i = 0; i < 16; ++i) flds[kR32Rg * w + 64 * i + lane] = c[i];
         R32_STAMP(16);
         __syncthreads();
         R32_STAMP(17);
@@ -541,7 +620,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int home = hi ? r32_column_home(16 + r) : r32_column_home(r); // uniform
-                a[r] = flds[1024 * (home >> 2) + 16 * (home & 3) + base];
+                a[r] = flds[kR32Rg * (home >> 2) + 16 * (home & 3) + base];
             }
         }
         R32_STAMP(18);
@@ -549,9 +628,9 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
         R32_STAMP(19);
         {
             // registers 16..31: beta = i + 16 (1 - h) -> thread 16 beta + gam's region
-            const int base = 4096 * (1 - h) + 64 * (k1 & 15) + gam;
+            const int base = 4 * kR32Rg * (1 - h) + 64 * (k1 & 15) + gam;
 #pragma unroll
-            for (int i = 0; i < 16; ++i) flds[base + 1024 * (i >> 2) + 16 * (i & 3)] = c[16 + i];
+            for (int i = 0; i < 16; ++i) flds[base + kR32Rg * (i >> 2) + 16 * (i & 3)] = c[16 + i];
         }
         if (LCFIR_R32_REGLOAD) {
             // the next unit's samples, in flight across the last barrier and
@@ -565,7 +644,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
         __syncthreads();
         if (LCFIR_R32_PRIO == 2 && hi) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) a[16 + i] = flds[1024 * w + 64 * i + lane];
+        for (int i = 0; i < 16; ++i) a[16 + i] = flds[kR32Rg * w + 64 * i + lane];
         R32_STAMP(21);
         // vmcnt(0) lgkmcnt(0): the wave's reads of its region have retired (and
         // the compiler's vmcnt accounting ignores LDS-DMA; see fir_fft32.hpp)

@@ -104,11 +104,11 @@ def check_read(slots, what, conflicts):
 # ---- the LDS image ----------------------------------------------------------------
 class Lds:
     def __init__(self):
-        self.v = np.full(8192, np.nan + 1j * np.nan)
-        self.tag = [None] * 8192
+        self.v = np.full(8 * RG, np.nan + 1j * np.nan)
+        self.tag = [None] * (8 * RG)
 
     def write(self, slot, val, tag):
-        assert 0 <= slot < 8192
+        assert 0 <= slot < 8 * RG
         self.v[slot] = val
         self.tag[slot] = tag
 
@@ -118,8 +118,17 @@ class Lds:
 
 
 # T2 (wave-local, both rounds): (g, h, kappa_local, gamma) in wave w's region
+# the kernel's LDS layout (fir_fft32r.hpp, LCFIR_R32_PAD = 1): one region of
+# RG slots per wave; T2 rows padded to 17 slots (a reader's addresses are its
+# row base + register index, conflict-free without a swizzle)
+PAD = True
+RG = 1088 if PAD else 1024
+
+
 def t2_slot(w, g, h, kl, gamma):
-    return 1024 * w + 512 * g + 256 * h + 16 * kl + (gamma ^ kl)
+    if PAD:
+        return RG * w + 544 * g + 272 * h + 17 * kl + gamma
+    return RG * w + 512 * g + 256 * h + 16 * kl + (gamma ^ kl)
 
 
 def dft(v, axis=-1):
@@ -160,8 +169,16 @@ def bin_of(k1, kap, lam):
     return k1 + 32 * kap + 1024 * lam
 
 
-def run(taps, x_seg):
+def run(taps, x_seg, tables=None):
+    """One unit of the kernel on segment x_seg.  tables: the host's plan
+    tables (fft_tables_dump, fft32_model.load_tables) -- task words, pair
+    coefficients per (thread, slot) and c8 -- instead of this model's own."""
     conflicts = []
+    tasks = t2_tasks
+    if tables is not None:
+        def tasks(w, g, s):  # noqa: F811  (r32_task_word's bit fields)
+            tk = int(tables["task"][64 * w + 32 * g + s])
+            return (tk & 1, (tk >> 1) & 15), ((tk >> 5) & 1, 16 + ((tk >> 6) & 15))
     z = x_seg[0::2] + 1j * x_seg[1::2]
     # ---- stage 1: thread b, register n; waves 4..7 (sigma = 1) negate the odd
     # inputs, so register r holds k1 = (r + 16 sigma) mod 32: registers 0..15
@@ -182,7 +199,7 @@ def run(taps, x_seg):
             slots = []
             for lane in range(64):
                 b = 64 * w + lane
-                s_ = 1024 * w + 64 * i + lane
+                s_ = RG * w + 64 * i + lane
                 lds.write(s_, reg1[b][i], ("t1", b, k1_of(i, int(b >= 256))))
                 slots.append(s_)
             check_write(slots, f"T1w1 w{w} i{i}")
@@ -196,7 +213,7 @@ def run(taps, x_seg):
                 assert (k1 >= 16) == bool(h)
                 beta = i + 16 * h
                 b = 16 * beta + gamma
-                s_ = 1024 * (b >> 6) + 64 * (k1 & 15) + (b & 63)
+                s_ = RG * (b >> 6) + 64 * (k1 & 15) + (b & 63)
                 col.setdefault((k1, gamma), [None] * 32)[i] = lds.read(s_, ("t1", b, k1))
                 slots.append(s_)
             check_read(slots, f"T1r1 w{w}", conflicts)
@@ -209,7 +226,7 @@ def run(taps, x_seg):
                 b = 64 * w + lane
                 k1 = k1_of(16 + i, int(b >= 256))
                 cw, cg, ch = COL_OF[k1]
-                s_ = 1024 * cw + 256 * (2 * cg + ch) + 16 * ((b >> 4) & 15) + (b & 15)
+                s_ = RG * cw + 256 * (2 * cg + ch) + 16 * ((b >> 4) & 15) + (b & 15)
                 lds.write(s_, reg1[b][16 + i], ("t1", b, k1))
                 slots.append(s_)
             check_write(slots, f"T1w2 w{w} i{i}")
@@ -221,7 +238,7 @@ def run(taps, x_seg):
                 k1 = column(w, g, h)
                 beta = i + 16 * (1 - h)
                 b = 16 * beta + gamma
-                s_ = 1024 * w + 256 * (2 * g + h) + 16 * i + gamma
+                s_ = RG * w + 256 * (2 * g + h) + 16 * i + gamma
                 col[(k1, gamma)][16 + i] = lds.read(s_, ("t1", b, k1))
                 slots.append(s_)
             check_read(slots, f"T1r2 w{w}", conflicts)
@@ -251,7 +268,7 @@ def run(taps, x_seg):
                 slots = []
                 for lane in range(64):
                     g, s_ = lane >> 5, lane & 31
-                    h, kap = t2_tasks(w, g, s_)[rnd]
+                    h, kap = tasks(w, g, s_)[rnd]
                     assert (kap >= 16) == (rnd == 1)
                     k1 = column(w, g, h)
                     s = t2_slot(w, g, h, kap - 16 * rnd, i)
@@ -266,15 +283,22 @@ def run(taps, x_seg):
         for rnd, reg in enumerate((r1, r2)):
             out = dft(np.array(reg))
             R[(w, g, s_)][rnd] = out
-            h, kap = t2_tasks(w, g, s_)[rnd]
+            h, kap = tasks(w, g, s_)[rnd]
             k1 = column(w, g, h)
             err = max(err, np.max(np.abs(out - Zref[bin_of(k1, kap, np.arange(16))])))
     assert err < 1e-6 * np.max(np.abs(Zref)), err
     # ---- pair step: slot i pairs P = x[i], Q = y[15 - i]; table by P's bin
-    p1, q2, p2, c8 = pair_tables(taps)
+    p1, q2, p2, c8 = pair_tables(taps) if tables is None else (None, None, None, tables["c8"][0].real)
+
+    def coef(t, i, k):
+        if tables is None:
+            return p1[k], q2[k], p2[k]
+        pq = tables["pair"][i * NT + t]
+        pp = tables["pair"][(16 + i // 2) * NT + t]
+        return pq.real, pq.imag, (pp.imag if i & 1 else pp.real)
     for (w, g, s_), (r1, r2) in R.items():
         x, y = list(r1), list(r2)
-        (h1, kap1), (h2, kap2) = t2_tasks(w, g, s_)
+        (h1, kap1), (h2, kap2) = tasks(w, g, s_)
         bx = [bin_of(column(w, g, h1), kap1, lam) for lam in range(16)]
         by = [bin_of(column(w, g, h2), kap2, lam) for lam in range(16)]
         special = (w, g, s_) == SPECIAL
@@ -287,7 +311,7 @@ def run(taps, x_seg):
         for i in range(16):
             kP, kQ = bx[i], by[15 - i]
             assert (kP + kQ) % N == 0, (w, g, s_, i, kP, kQ)
-            x[i], y[15 - i] = pair_sym(x[i], y[15 - i], p1[kP], q2[kP], p2[kP])
+            x[i], y[15 - i] = pair_sym(x[i], y[15 - i], *coef(64 * w + 32 * g + s_, i, kP))
         if special:
             o8 = np.conj(v8 * c8)
             # inverse permutation (slot 15's Q output, a duplicate of bin 0's, is dropped)
@@ -307,7 +331,7 @@ def run(taps, x_seg):
                 slots = []
                 for lane in range(64):
                     g, s_ = lane >> 5, lane & 31
-                    h, kap = t2_tasks(w, g, s_)[rnd]
+                    h, kap = tasks(w, g, s_)[rnd]
                     s = t2_slot(w, g, h, kap - 16 * rnd, i)
                     lds.write(s, R[(w, g, s_)][rnd][i], ("t2i", w, g, h, kap, i))
                     slots.append(s)
@@ -340,7 +364,7 @@ def run(taps, x_seg):
                 g, h, gamma = lane >> 5, (lane >> 4) & 1, lane & 15
                 k1 = column(w, g, h)
                 beta = i + 16 * h
-                s_ = 1024 * w + 64 * i + lane
+                s_ = RG * w + 64 * i + lane
                 lds.write(s_, U2[(k1, gamma)][i], ("t1i", 16 * beta + gamma, k1))
                 slots.append(s_)
             check_write(slots, f"T1'w1 w{w}")
@@ -353,7 +377,7 @@ def run(taps, x_seg):
                 k1 = k1_of(r, sig)
                 cw, cg, ch = COL_OF[k1]
                 beta, gamma = b >> 4, b & 15
-                s_ = 1024 * cw + 64 * (beta & 15) + 32 * cg + 16 * ch + gamma
+                s_ = RG * cw + 64 * (beta & 15) + 32 * cg + 16 * ch + gamma
                 fin[b][r] = lds.read(s_, ("t1i", b, k1))
                 slots.append(s_)
             check_read(slots, f"T1'r1 w{w}", conflicts)
@@ -367,7 +391,7 @@ def run(taps, x_seg):
                 k1 = column(w, g, h)
                 beta = (16 + i + 16 * h) % 32
                 b = 16 * beta + gamma
-                s_ = 1024 * (b >> 6) + 64 * (k1 & 15) + (b & 63)
+                s_ = RG * (b >> 6) + 64 * (k1 & 15) + (b & 63)
                 lds.write(s_, U2[(k1, gamma)][16 + i], ("t1i", b, k1))
                 slots.append(s_)
             check_write(slots, f"T1'w2 w{w}")
@@ -377,7 +401,7 @@ def run(taps, x_seg):
             for lane in range(64):
                 b = 64 * w + lane
                 k1 = k1_of(16 + i, int(b >= 256))
-                s_ = 1024 * w + 64 * i + lane
+                s_ = RG * w + 64 * i + lane
                 fin[b][16 + i] = lds.read(s_, ("t1i", b, k1))
                 slots.append(s_)
             check_read(slots, f"T1'r2 w{w}", conflicts)
@@ -395,8 +419,9 @@ def run(taps, x_seg):
     return c, conflicts
 
 
-def main():
-    ntaps = int(sys.argv[1]) if len(sys.argv) > 1 else 8001
+def main(ntaps=None):
+    if ntaps is None:
+        ntaps = int(sys.argv[1]) if len(sys.argv) > 1 else 8001
     rng = np.random.default_rng(5)
     half = (ntaps - 1) // 2
     n = np.arange(ntaps) - half

@@ -4,7 +4,7 @@
 //
 // usage: fft_tables_dump taps.f64 seg_len zero_phase out_prefix
 // (seg_len 0: the library's own choice for the taps, fft_choose_seg_len)
-// writes <out_prefix>.meta (L halves parts tp sym, text), .pair .c8 .tw
+// writes <out_prefix>.meta (L halves parts tp sym reg32, text), .pair .c8 .tw
 // (complex double pairs) and .task (uint32).
 #include <cstdio>
 #include <cstdlib>
@@ -36,7 +36,8 @@ int main(int argc, char **argv) {
     const lcfir::FftTables T = lcfir::fft_plan_tables(taps, tune);
     const std::string out = argv[4];
     std::ofstream m(out + ".meta");
-    m << T.L << " " << T.halves << " " << T.parts << " " << T.tp << " " << (T.sym ? 1 : 0) << "\n";
+    m << T.L << " " << T.halves << " " << T.parts << " " << T.tp << " " << (T.sym ? 1 : 0) << " "
+      << (T.reg32 ? 1 : 0) << "\n";
     dump(out + ".pair", T.pair);
     dump(out + ".task", T.task);
     dump(out + ".c8", T.c8);

@@ -17,6 +17,7 @@ from conftest import ROOT
 
 sys.path.insert(0, os.path.join(ROOT, "scripts"))
 import fft32_model as fm  # noqa: E402
+import fft32r_model as rm  # noqa: E402
 
 DUMP = os.path.join(ROOT, "tests", "cpp", "fft_tables_dump")
 
@@ -31,6 +32,14 @@ def test_model_against_convolution():
     fm.main()
 
 
+def test_register_kernel_model_against_convolution():
+    """scripts/fft32r_model.py: fir_fft32r_kernel's data flow (every register
+    index, LDS slot of both exchanges and their rounds, the special lane's
+    permutation) with its own tables, against direct convolution; no LDS read
+    bank conflicts."""
+    rm.main(8001)
+
+
 @pytest.mark.parametrize("seg_len,ntaps,sym", [(32768, 8001, True), (32768, 4001, True), (32768, 4003, False),
                                                (32768, 8001, False), (32768, 19201, True), (16384, 4001, True),
                                                (16384, 4003, False)])
@@ -43,9 +52,15 @@ def test_tables_emulated_segment(dump, tmp_path, seg_len, ntaps, sym):
     subprocess.run([dump, str(tmp_path / "t.f64"), str(seg_len), "1", str(tmp_path / "tb")], check=True)
     tb = fm.load_tables(str(tmp_path / "tb"))
     assert tb["L"] == seg_len and tb["parts"] == 1 and tb["sym"] == sym
+    # zero-phase single-partition L = 32 768 plans run the register kernel
+    assert tb["reg32"] == (seg_len == 32768 and sym)
     rng = np.random.default_rng(ntaps)
     x = rng.uniform(-1, 1, seg_len)
-    c = fm.emulate(x, tb)
+    if tb["reg32"]:  # the register kernel's flow on the host's task words and pair table
+        c, conflicts = rm.run(taps, x, tables=tb)
+        assert not conflicts
+    else:
+        c = fm.emulate(x, tb)
     half = (ntaps - 1) // 2
     if tb["sym"]:
         ms = np.arange(half, seg_len - half, 509)  # c[m] = sum_k h[k] x[m - half + k]
@@ -59,18 +74,25 @@ def test_tables_emulated_segment(dump, tmp_path, seg_len, ntaps, sym):
 
 def test_seg_len_choice(dump, tmp_path):
     """fft_choose_seg_len (measured unit costs): a function of
-    the taps alone, the per-output cost decides -- 16 384 up to config 3's
-    8 001 taps, 32 768 from 10 001 (one unit 2.9x an L = 16 384 one for 3.6x
-    the outputs), for 19 201 (one partition instead of two; config 1's filter)
-    and 38 401 (two instead of five)."""
+    the taps alone, the per-output cost decides.  Linear-phase filters: the
+    register kernel's L = 32 768 unit costs 2.2 L = 16 384 units, so 16 384 up
+    to ~4 000 taps and 32 768 from config 2's 4 001 (7.65e-5 against 8.07e-5
+    per output); 38 401 taps take two L = 32 768 partitions (the park-slab
+    kernel, 4.0) instead of five.  Other filters (the general table): the
+    park-slab kernel (3.1), 16 384 up to 8 001 taps, 32 768 from 10 001."""
     import oracle
-    cases = [(401, 16384, 1), (4001, 16384, 1), (8001, 16384, 1), (10001, 32768, 1), (12001, 32768, 1),
-             (19201, 32768, 1), (38401, 32768, 2)]
-    for ntaps, L, parts in cases:
-        oracle.design_lowcut(20.0, 48000.0, ntaps).tofile(tmp_path / "t.f64")
+    cases = [(401, True, 16384, 1), (3001, True, 16384, 1), (4001, True, 32768, 1), (8001, True, 32768, 1),
+             (19201, True, 32768, 1), (38401, True, 32768, 2),
+             (4001, False, 16384, 1), (8001, False, 16384, 1), (10001, False, 32768, 1), (19201, False, 32768, 1)]
+    for ntaps, sym, L, parts in cases:
+        taps = oracle.design_lowcut(20.0, 48000.0, ntaps)
+        if not sym:
+            taps = taps + 1e-3 * np.linspace(-1.0, 1.0, ntaps)
+        taps.tofile(tmp_path / "t.f64")
         subprocess.run([dump, str(tmp_path / "t.f64"), "0", "1", str(tmp_path / "tb")], check=True)
         tb = fm.load_tables(str(tmp_path / "tb"))
-        assert (tb["L"], tb["parts"]) == (L, parts), ntaps
+        assert (tb["L"], tb["parts"], tb["sym"]) == (L, parts, sym and parts == 1), ntaps
+        assert tb["reg32"] == (L == 32768 and parts == 1 and sym), ntaps
 
 
 def test_header_constants_match_model():

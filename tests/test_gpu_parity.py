@@ -610,14 +610,16 @@ def test_fft_seg32_chunks_and_groups(lc, oracle_mod):
 
 
 @pytest.mark.parametrize("ntaps,n,nch,want_L", [(12001, 3_000_000, 2, 32768), (19201, 48_000, 1, 32768),
-                                                (8001, 600_000, 8, 16384)])
+                                                (8001, 600_000, 8, 32768), (4001, 600_000, 2, 32768),
+                                                (3001, 600_000, 2, 16384)])
 def test_fft_auto_seg_len(lc, oracle_mod, ntaps, n, nch, want_L):
     """The automatic segment length (fir_fft.hpp fft_choose_seg_len), a
-    function of the taps: long filters take the L = 32 768 segment (12 001
-    taps: one partition instead of two; config 1's 19 201 taps on its short
-    channel too), and 8 001 taps (even costs) stays at 16 384.  The product
-    path as it runs by default, against the long-double oracle at every edge
-    sample and random positions, fused peaks."""
+    function of the taps: linear-phase filters from ~4 000 taps take the
+    L = 32 768 segment on the register kernel (config 2's 4 001, config 3's
+    8 001; 12 001 taps: one partition instead of two; config 1's 19 201 taps
+    on its short channel too), 3 001 taps stay at 16 384.  The product path as
+    it runs by default, against the long-double oracle at every edge sample
+    and random positions, fused peaks."""
     import synth
     fs = 48000.0
     taps = oracle_mod.design_lowcut(20.0, fs, ntaps)
