@@ -1616,18 +1616,28 @@ inline int64_t fft_chunk(const FftPlan &plan) {
 // work array + twiddles + 8 f32 peak slots + the special lane's 32 double2
 constexpr size_t kR32LdsBytes = sizeof(double2) * (size_t)(kR32Work + kR32Tw + 2 + 32);
 
-template <int kOut>
-inline bool fft32r_launch_one(const FftPlan &plan, const DirectParams &q, int nch, hipStream_t s, std::string &err) {
+template <int kOut, bool kNrm = false>
+inline bool fft32r_launch_one(const FftPlan &plan, const DirectParams &q, int nch, hipStream_t s, std::string &err,
+                              FftNrm nrm = FftNrm{}) {
     static const bool attr = [] {
-        return hipFuncSetAttribute(reinterpret_cast<const void *>(&fir_fft32r_kernel<kOut>),
+        return hipFuncSetAttribute(reinterpret_cast<const void *>(&fir_fft32r_kernel<kOut, kNrm>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kR32LdsBytes) == hipSuccess;
     }();
     (void)attr;
     const int64_t nseg = (q.end - q.seg0 + plan.B - 1) / plan.B;
     const int64_t units = nseg * nch; // < 2^31 (fft_launch)
     const int64_t grid = std::min<int64_t>(units, (int64_t)plan.cus);
-    hipLaunchKernelGGL(fir_fft32r_kernel<kOut>, dim3((unsigned)grid), dim3(kFftNT), kR32LdsBytes, s, q, plan.d_pair,
-                       plan.d_tw, plan.d_task, plan.B, fft_grid(nseg, units), plan.c8[0].x);
+    if constexpr (kNrm) {
+        // whole 2 048-float blocks per unit (two halves of <= kNrmK x 1 024, fft_nrm_fusable)
+        const int64_t per = (nrm.count + units - 1) / units;
+        nrm.slice = (per + 2047) / 2048 * 2048;
+        if (nrm.slice > (int64_t)kNrmK * 2048) {
+            err = "normalize slice too large to fuse";
+            return false;
+        }
+    }
+    hipLaunchKernelGGL((fir_fft32r_kernel<kOut, kNrm>), dim3((unsigned)grid), dim3(kFftNT), kR32LdsBytes, s, q,
+                       plan.d_pair, plan.d_tw, plan.d_task, plan.B, fft_grid(nseg, units), plan.c8[0].x, nrm);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         err = hipGetErrorString(e);
@@ -1668,6 +1678,8 @@ inline bool fft32_launch_one(const FftPlan &plan, const DirectParams &q, int par
 template <int kOut, bool kNrm = false>
 inline bool fft_launch_one(const FftPlan &plan, const DirectParams &q, int part, int nch, hipStream_t s,
                            std::string &err, FftNrm nrm = FftNrm{}) {
+    if constexpr (kOut == kFftOutSym)
+        if (plan.reg32) return fft32r_launch_one<kOut, kNrm>(plan, q, nch, s, err, nrm);
     if constexpr (!kNrm)
         if (plan.L == kFft32L) return fft32_launch_one<kOut>(plan, q, part, nch, s, err);
     static const bool attr = [] {
@@ -1762,19 +1774,21 @@ inline int64_t fft_max_units(const FftPlan &plan) {
 inline bool fft_launch_group(const FftPlan &plan, const DirectParams &p, int nch, hipStream_t s,
                              std::string &err, const FftNrm *nrm);
 // Can fft_launch carry a previous file's normalize (FftNrm) in its first
-// launch?  Single-partition filters on the default kernel, 16-B aligned
-// buffer; otherwise the caller runs the normalize pass itself.
-// The first launch (the one that carries it) must spread the previous
-// file's floats at <= kNrmK x 1 024 per unit.
+// launch?  Single-partition filters on the L = 16 384 or the register-resident
+// L = 32 768 kernel, 16-B aligned buffer; otherwise the caller runs the
+// normalize pass itself.  The first launch (the one that carries it) must
+// spread the previous file's floats at <= kNrmK x 1 024 per unit (x 2 048 on
+// the register kernel: two halves).
 inline bool fft_nrm_fusable(const FftPlan &plan, const FftNrm &nrm, const DirectParams &p, int nch) {
-    if (plan.parts != 1 || plan.L != kFftL || !nrm.y || !nrm.peak || nrm.npeak < 1 ||
+    if (plan.parts != 1 || (plan.L != kFftL && !plan.reg32) || !nrm.y || !nrm.peak || nrm.npeak < 1 ||
         (reinterpret_cast<uintptr_t>(nrm.y) & 15) != 0 || p.end <= p.start || nch <= 0)
         return false;
     const int64_t nseg = fft_first_nseg(plan, p);
     const int64_t group = std::max<int64_t>(1, std::min<int64_t>(nch, fft_max_units(plan) / nseg));
     const int64_t units = nseg * group;
     const int64_t per = (nrm.count + units - 1) / units;
-    return (per + 1023) / 1024 <= kNrmK;
+    // fir_fft32r_kernel takes two halves of up to kNrmK x 1 024 floats per unit
+    return plan.reg32 ? (per + 2047) / 2048 <= kNrmK : (per + 1023) / 1024 <= kNrmK;
 }
 // nrm: a previous file's normalize to fuse (fft_nrm_fusable must hold), or null
 inline bool fft_launch(const FftPlan &plan, const DirectParams &p, int nch, hipStream_t s,

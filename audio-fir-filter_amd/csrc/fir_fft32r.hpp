@@ -48,14 +48,8 @@ constexpr int kR32TwG = 1024;   // W_512^g, g < 16
 constexpr int kR32Tw = 1024 + 16;
 constexpr size_t kR32PairTable = (size_t)24 * kFftNT; // double2: (p1, q2) [16][512], (p2 even, p2 odd) [8][512]
 constexpr int kR32SpecialLane = 31;                   // of wave 0
-#ifndef LCFIR_R32_REGLOAD
-#define LCFIR_R32_REGLOAD 0 // 1: the next unit's samples by register loads issued in T1 backwards (no LDS-DMA)
-#endif
 #ifndef LCFIR_R32_PAD
 #define LCFIR_R32_PAD 1 // T2's rows padded to 17 slots: conflict-free without an XOR swizzle's address math (-5 %)
-#endif
-#ifndef LCFIR_R32_PRIO
-#define LCFIR_R32_PRIO 0 // tools builds: issue priority of waves 4..7 (1 always, 2 BAR6..BAR1, 3 BAR3..BAR4)
 #endif
 
 // Phase timestamps for tools/fft32r_trace.hip (off in the product build):
@@ -268,6 +262,54 @@ __device__ __forceinline__ void r32_chain32(double2 (&a)[32], double2 w) {
     }
 }
 
+#ifndef LCFIR_R32_TW
+#define LCFIR_R32_TW 1 // twiddle powers: 1 = anchored chains (~2e-15), 0 = plain Chebyshev recurrence (~6e-14)
+#endif
+// a[off + r] *= s0 w^r, r < R (a multiple of 4), for a unit w, w4 = w^4:
+// anchors A = s0 w^(4m) by complex multiplies, and from each anchor two
+// Chebyshev steps s_(r+1) = 2 Re(w) s_r - s_(r-1) (two FMAs a power).  The
+// plain recurrence over 31 powers amplifies rounding to ~6e-14 for small
+// angles -- 14 f32 ulps at config 3's smallest outputs; two steps from an
+// anchor stay at the chains' ~2e-15.  Each power is applied as it is made.
+template <int R>
+__device__ __forceinline__ void r32_chain_anchored(double2 (&a)[32], int off, double2 s0, double2 w, double2 w4) {
+    const double c2 = w.x + w.x;
+    double2 A = s0;
+#pragma unroll
+    for (int m = 0; m < R / 4; ++m) {
+        const double2 p1 = cmul(A, w);
+        const double2 p2 = make_double2(__builtin_fma(c2, p1.x, -A.x), __builtin_fma(c2, p1.y, -A.y));
+        const double2 p3 = make_double2(__builtin_fma(c2, p2.x, -p1.x), __builtin_fma(c2, p2.y, -p1.y));
+        a[off + 4 * m] = cmul(a[off + 4 * m], A);
+        a[off + 4 * m + 1] = cmul(a[off + 4 * m + 1], p1);
+        a[off + 4 * m + 2] = cmul(a[off + 4 * m + 2], p2);
+        a[off + 4 * m + 3] = cmul(a[off + 4 * m + 3], p3);
+        if (m + 1 < R / 4) A = cmul(A, w4);
+    }
+}
+// a[r] *= w^r, r < 32
+__device__ __forceinline__ void r32_chain32acc(double2 (&a)[32], double2 w) {
+    const double2 w2 = cmul(w, w);
+    const double2 w4 = cmul(w2, w2);
+    const double c2 = w.x + w.x;
+    // anchor 0 is 1: its powers w, 2 Re(w) w - 1, ...
+    const double2 p2 = make_double2(__builtin_fma(c2, w.x, -1.0), c2 * w.y);
+    const double2 p3 = make_double2(__builtin_fma(c2, p2.x, -w.x), __builtin_fma(c2, p2.y, -w.y));
+    a[1] = cmul(a[1], w);
+    a[2] = cmul(a[2], p2);
+    a[3] = cmul(a[3], p3);
+    r32_chain_anchored<28>(a, 4, w4, w, w4);
+}
+// stage 1 / final: register r holds k1 = r + 16 hi (mod 32): registers 0..15
+// take s0 w^r, 16..31 s1 w^(r-16), {s0, s1} = {1, w16} (w16 = W_1024^b, a table value)
+__device__ __forceinline__ void r32_chain_k1acc(double2 (&a)[32], double2 w, double2 w16, bool hi) {
+    const double2 w2 = cmul(w, w);
+    const double2 w4 = cmul(w2, w2);
+    const double2 one = make_double2(1.0, 0.0);
+    r32_chain_anchored<16>(a, 0, csel(hi, w16, one), w, w4);
+    r32_chain_anchored<16>(a, 16, csel(hi, one, w16), w, w4);
+}
+
 // Samples of unit (ch, n0) into wave w's region flds[1024 w, + 1024) as the
 // float2 z[512 n + 64 w + i] at float2 index 2048 w + 64 n + i (the caller
 // has retired the wave's reads of its region).  Interior units by LDS-DMA
@@ -361,34 +403,66 @@ __device__ __forceinline__ float r32_store_unit(const DirectParams &p, int ch, i
     return pk;
 }
 
+// The kernel's workgroup barriers order LDS only: __syncthreads()'s release
+// fence would also wait for the wave's global stores (the previous unit's
+// outputs, a fused normalize slice), which no other wave reads.
+__device__ __forceinline__ void r32_bar() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // Persistent, XCD-aware grid as fir_fft_f64_kernel (one 512-thread workgroup
 // per CU, fft_unit32), zero-phase single-partition filters (kFftOutSym).
 // pair: kR32PairTable (fft_plan_tables); tw: kR32Tw twiddles; task: 512
 // r32_task_word; c8: the special lane's bin-N/2 coefficient (real).
-template <int kOut = kFftOutSym> // a template, so host-only users of this header emit no kernel stub
+// kNrm: the launch also rescales a previous file's outputs (FftNrm, as
+// fir_fft_f64_kernel): unit u's slice is two halves, 2u and 2u + 1 of slice / 2
+// floats, which the older waves (0..3) load, rescale and store while they
+// wait at T1's first barrier and at T1 backwards' first barrier (the younger
+// waves arrive there thousands of cycles later).
+template <int kOut = kFftOutSym, bool kNrm = false> // templates: host-only users emit no kernel stub
 __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, const double2 *__restrict__ pair,
                                                            const double2 *__restrict__ tw,
                                                            const uint32_t *__restrict__ task, int B, FftGrid gd,
-                                                           double c8) {
+                                                           double c8, FftNrm nrm) {
     extern __shared__ double2 flds[];
+    bool nrm_on = false;
+    double nrm_gain = 1.0;
+    if constexpr (kNrm) {
+        float pkv = 0.0f;
+        for (int i = 0; i < nrm.npeak; ++i) pkv = fmaxf(pkv, __uint_as_float(nrm.peak[i]));
+        nrm_on = (pkv > 1.0f || nrm.force) && pkv > 0.0f;
+        nrm_gain = 1.0 / (double)pkv;
+        __builtin_amdgcn_s_setprio(1); // the older waves drop to 0 for their slices
+    }
+    // half h of unit u's normalize slice, by the older waves, at priority 0
+    auto nrm_half = [&](int u, int h, int j, int wu) {
+        if constexpr (kNrm) {
+            if (nrm_on && wu < 4) {
+                __builtin_amdgcn_s_setprio(0);
+                FftNrm nh = nrm;
+                nh.slice = nrm.slice / 2;
+                float4 nv[kNrmK];
+                fft_nrm_load(nh, 2 * u + h, j, true, nv);
+                fft_nrm_store(nh, 2 * u + h, j, nrm_gain, nv);
+                __builtin_amdgcn_s_setprio(1);
+            }
+        }
+    };
     double2 *twl = flds + kR32Work; // kR32Tw twiddles, then 8 f32 peak slots, then the special lane's scratch
     for (int i = threadIdx.x; i < kR32Tw; i += kFftNT) twl[i] = tw[i];
     float *pk_lds = reinterpret_cast<float *>(twl + kR32Tw);
     double2 *spl = twl + kR32Tw + 2;
-    float2 v[32]; // LCFIR_R32_REGLOAD: the samples of the unit about to start
     {
         const int u = fft_unit32(0, blockIdx.x, gridDim.x, gd.units);
         const int c = fft_div(u, gd);
-        if (LCFIR_R32_REGLOAD)
-            fft_load_unit<32>(p, c, p.seg0 + (int64_t)(u - c * gd.nseg) * B, threadIdx.x, v);
-        else
-            r32_stage_samples(p, c, p.seg0 + (int64_t)(u - c * gd.nseg) * B, threadIdx.x, flds);
+        r32_stage_samples(p, c, p.seg0 + (int64_t)(u - c * gd.nseg) * B, threadIdx.x, flds);
     }
     __builtin_amdgcn_s_waitcnt(kVmcnt0);
     __syncthreads();
     uint32_t tk_all = task[threadIdx.x];
     asm volatile("" : "+v"(tk_all));
-    if (LCFIR_R32_PRIO == 1 && __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= 4) __builtin_amdgcn_s_setprio(1);
     float pk_run = 0.0f;
     int pk_ch = -1;
     int pk_pending = -1;
@@ -411,7 +485,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
             const int sg = hi ? (int)0x80000000 : 0;
 #pragma unroll
             for (int n = 0; n < 32; ++n) {
-                float2 vn = LCFIR_R32_REGLOAD ? v[n] : fz[64 * n];
+                float2 vn = fz[64 * n];
                 if (n & 1) {
                     vn.x = __int_as_float(__float_as_int(vn.x) ^ sg);
                     vn.y = __int_as_float(__float_as_int(vn.y) ^ sg);
@@ -423,8 +497,12 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
         {
             // register r holds k1 = r + 16 hi (mod 32): powers w^(16 hi) w^r, w^(16 (1 - hi)) w^(r - 16)
             const double2 wb = twl[kR32TwB + j], w16 = twl[kR32TwB16 + j], one = make_double2(1.0, 0.0);
-            r32_chain16(a, 0, csel(hi, w16, one), wb);
-            r32_chain16(a, 16, csel(hi, one, w16), wb);
+            if (LCFIR_R32_TW) {
+                r32_chain_k1acc(a, wb, w16, hi);
+            } else {
+                r32_chain16(a, 0, csel(hi, w16, one), wb);
+                r32_chain16(a, 16, csel(hi, one, w16), wb);
+            }
         }
         R32_STAMP(1);
         // ---- T1 round 1: registers 0..15 into the wave's own region (its lanes
@@ -432,9 +510,9 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
 #pragma unroll
         for (int i = 0; i < 16; ++i) flds[kR32Rg * w + 64 * i + lane] = a[i];
         R32_STAMP(2);
-        __syncthreads();
+        nrm_half(u, 0, j, wu);
+        r32_bar();
         R32_STAMP(3);
-        if (LCFIR_R32_PRIO == 2 && hi) __builtin_amdgcn_s_setprio(0);
         if (pk_pending >= 0) {
             if (threadIdx.x == 0) fft_peak_commit(p, pk_pending, pk_lds);
             pk_pending = -1;
@@ -449,7 +527,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
             for (int i = 0; i < 16; ++i) c[i] = flds[base + kR32Rg * (i >> 2) + 16 * (i & 3)];
         }
         R32_STAMP(4);
-        __syncthreads();
+        r32_bar();
         R32_STAMP(5);
         // ---- T1 round 2: registers 16..31 (k1 = 16 + i, or i for waves 4..7)
         // into the region of their column's wave
@@ -462,8 +540,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
             }
         }
         R32_STAMP(6);
-        __syncthreads();
-        if (LCFIR_R32_PRIO == 3 && hi) __builtin_amdgcn_s_setprio(1);
+        r32_bar();
         {
             const int base = kR32Rg * w + 256 * (2 * g + h) + gam;
 #pragma unroll
@@ -474,7 +551,10 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
         dft32(c);
         double2 wg = twl[kR32TwG + gam];
         if (h) wg = make_double2(-wg.x, -wg.y);
-        r32_chain32(c, wg);
+        if (LCFIR_R32_TW)
+            r32_chain32acc(c, wg);
+        else
+            r32_chain32(c, wg);
         R32_STAMP(8);
         // ---- the pair table's first half, in flight across T2
         double2 pq[16], p2v[8];
@@ -603,7 +683,10 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
         // The powers are rebuilt, not kept from stage 2 (124 VGPRs across the
         // pair step): the laundered base stops the compiler from reusing them.
         asm volatile("" : "+v"(wg.x), "+v"(wg.y));
-        r32_chain32(c, wg);
+        if (LCFIR_R32_TW)
+            r32_chain32acc(c, wg);
+        else
+            r32_chain32(c, wg);
         dft32(c);
         wave_lds_sync();
         R32_STAMP(15);
@@ -611,9 +694,9 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
 #pragma unroll
         for (int i = 0; i < 16; ++i) flds[kR32Rg * w + 64 * i + lane] = c[i];
         R32_STAMP(16);
-        __syncthreads();
+        nrm_half(u, 1, j, wu);
+        r32_bar();
         R32_STAMP(17);
-        if (LCFIR_R32_PRIO == 3 && hi) __builtin_amdgcn_s_setprio(0);
         {
             // thread b: register r holds k1 = r + 16 hi, from lane (k1, gamma_b)'s register beta_b & 15
             const int base = 64 * ((j >> 4) & 15) + (j & 15);
@@ -624,7 +707,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
             }
         }
         R32_STAMP(18);
-        __syncthreads();
+        r32_bar();
         R32_STAMP(19);
         {
             // registers 16..31: beta = i + 16 (1 - h) -> thread 16 beta + gam's region
@@ -632,23 +715,14 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
 #pragma unroll
             for (int i = 0; i < 16; ++i) flds[base + kR32Rg * (i >> 2) + 16 * (i & 3)] = c[16 + i];
         }
-        if (LCFIR_R32_REGLOAD) {
-            // the next unit's samples, in flight across the last barrier and
-            // the final DFT (the last unit reloads itself)
-            const int un1 = fft_unit32(rnd + 1, blockIdx.x, gridDim.x, gd.units);
-            const int un = un1 < gd.units ? un1 : u;
-            const int cn = fft_div(un, gd);
-            fft_load_unit<32>(p, cn, p.seg0 + (int64_t)(un - cn * gd.nseg) * B, j, v);
-        }
         R32_STAMP(20);
-        __syncthreads();
-        if (LCFIR_R32_PRIO == 2 && hi) __builtin_amdgcn_s_setprio(1);
+        r32_bar();
 #pragma unroll
         for (int i = 0; i < 16; ++i) a[16 + i] = flds[kR32Rg * w + 64 * i + lane];
         R32_STAMP(21);
         // vmcnt(0) lgkmcnt(0): the wave's reads of its region have retired (and
         // the compiler's vmcnt accounting ignores LDS-DMA; see fir_fft32.hpp)
-        if (!LCFIR_R32_REGLOAD) {
+        {
             __builtin_amdgcn_s_waitcnt(0x0070);
             const int un1 = fft_unit32(rnd + 1, blockIdx.x, gridDim.x, gd.units);
             const int un = un1 < gd.units ? un1 : u;
@@ -659,8 +733,12 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
         // ---- final: * W_16384^(b k1), DFT32 over k1 -> n
         {
             const double2 wb = twl[kR32TwB + j], w16 = twl[kR32TwB16 + j], one = make_double2(1.0, 0.0);
-            r32_chain16(a, 0, csel(hi, w16, one), wb);
-            r32_chain16(a, 16, csel(hi, one, w16), wb);
+            if (LCFIR_R32_TW) {
+                r32_chain_k1acc(a, wb, w16, hi);
+            } else {
+                r32_chain16(a, 0, csel(hi, w16, one), wb);
+                r32_chain16(a, 16, csel(hi, one, w16), wb);
+            }
         }
         dft32(a);
         __builtin_amdgcn_s_waitcnt(kVmcnt0); // the staging transfers have landed (stage 1 reads them)

@@ -381,6 +381,15 @@ def preroll(step, seconds, sync, agree=None, batch=8):
     return steps
 
 
+
+def fft_kernel_name(info):
+    """The FFT kernel a plan runs (fir_fft.hpp fft_reg32): zero-phase
+    single-partition L = 32 768 plans the register-resident fir_fft32r_kernel,
+    other L = 32 768 plans fir_fft32_f64_kernel, L = 16 384 fir_fft_f64_kernel."""
+    if info["seg_len"] == 32768:
+        return "fir_fft32r_kernel" if info["parts"] == 1 and info["zero_phase"] else "fir_fft32_f64_kernel"
+    return "fir_fft_f64_kernel"
+
 def main():
     args = parse()
     if launch_plan(args.gpus, os.environ) == "spawn":
@@ -632,8 +641,7 @@ def main():
                 "frac_step_note": "4 B x samples per step per GPU / ms_per_step / 8 TB/s (whole step: "
                                   "launch gaps, collective, normalize passes, lane overlap included)",
                 "traffic": traffic,
-                "kernel": "fir_direct_f64_kernel" if method == "direct" else
-                          ("fir_fft32_f64_kernel" if flt.fft_info["seg_len"] == 32768 else "fir_fft_f64_kernel"),
+                "kernel": "fir_direct_f64_kernel" if method == "direct" else fft_kernel_name(flt.fft_info),
                 "kernel_ms": round(kern_ms, 6),
                 "kernel_ms_note": f"exclusive: {kern_launches} launches of the filter alone on one "
                                   f"stream right after the pre-roll (HIP events on that stream)",

@@ -36,7 +36,8 @@ def test_bench_json_line(lanes):
         assert k in r, k
     assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-5
-    assert r["kernel"] == "fir_fft_f64_kernel" and r["launches_timed"] == 5
+    # config 2's 4 001 linear-phase taps: the L = 32 768 register-resident kernel
+    assert r["kernel"] == "fir_fft32r_kernel" and r["launches_timed"] == 5
     # achieved = algorithmic read bytes of one launch / its exclusive duration
     assert abs(r["achieved"] - 4 * samples / (r["kernel_ms"] / 1e3) / 1e9) / r["achieved"] < 1e-3
     assert d["preroll"]["steps"] > 0

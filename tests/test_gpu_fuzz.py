@@ -151,11 +151,17 @@ def _norm_case(seed):
     method = "direct" if ntaps <= 1601 and rng.random() < 0.3 else "fft"
     nch = int(rng.integers(1, 4))
     n = int(rng.choice([1, 7, ntaps // 2 + 1, 20_000, 123_457, 300_001]))
-    # units of a one-partition FFT launch (B = L - T + 1, L = 16384; 19 201
-    # taps run as 2 x 9 601): counts around units * 14 Ki floats straddle the
-    # fused / separate-pass switch
-    B = 16384 - (ntaps if ntaps <= 10925 else 9601) + 1
-    boundary = -(-n // B) * nch * NRM_SLICE_MAX
+    # units of a one-partition FFT launch (B = L - T + 1): counts around
+    # units x the per-unit slice straddle the fused / separate-pass switch.
+    # Designed (linear-phase) filters from 4 001 taps run the register kernel
+    # (L = 32 768, two halves of 14 Ki floats per unit); the others L = 16 384
+    # (19 201 taps as 2 x 9 601)
+    designed = rng.random() < 0.6
+    if designed and ntaps >= 4001:
+        B, per_unit = 32768 - ntaps + 1, 2 * NRM_SLICE_MAX
+    else:
+        B, per_unit = 16384 - (ntaps if ntaps <= 10925 else 9601) + 1, NRM_SLICE_MAX
+    boundary = -(-n // B) * nch * per_unit
     count = int(rng.choice([
         1, 3, int(rng.integers(1, 5_000)), int(rng.integers(1, boundary + 1)),
         int(rng.integers(1, boundary + 1)), boundary, boundary + int(rng.integers(-8, 9)),
@@ -168,7 +174,6 @@ def _norm_case(seed):
     if rng.random() < 0.5:
         peaks[int(rng.integers(npeak))] = np.float32(rng.uniform(0.01, 4.0))
     force = bool(rng.random() < 0.4)
-    designed = rng.random() < 0.6
     return rng, ntaps, method, nch, n, count, offset, peaks, force, designed
 
 
