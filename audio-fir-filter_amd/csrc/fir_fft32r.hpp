@@ -593,31 +593,25 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
         R32_STAMP(11);
         // ---- pair step: slot i pairs R1[i] (bin k) with R2[15 - i] (bin N - k);
         // the special lane permutes its registers into that layout first
-        // (wave 0 only, a scalar branch; the special lane stores its registers
-        // under its own exec mask, then every lane of the wave reads the
-        // permuted values at wave-uniform addresses and the special lane keeps
-        // them by a per-lane select: no register is written under a divergent
-        // mask, which would cost every wave register copies around it)
-        const bool sp = lane == kR32SpecialLane;
-        const double2 v8 = R1[8];
+        const bool sp = wu == 0 && lane == kR32SpecialLane;
+        double2 v8 = R1[8];
         if (wu == 0) {
             if (sp) {
+                // x' = [R2 0..7, R1 1..7, R1 0], y' = [R1 0, R1 9..15, R2 8..15]; R1[8] (bin N/2) apart
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
                     spl[i] = R1[i];
                     spl[16 + i] = R2[i];
                 }
+#pragma unroll
+                for (int i = 0; i < 8; ++i) R1[i] = spl[16 + i];
+#pragma unroll
+                for (int i = 8; i < 15; ++i) R1[i] = spl[i - 7];
+                R1[15] = spl[0];
+                R2[0] = spl[0];
+#pragma unroll
+                for (int i = 1; i < 8; ++i) R2[i] = spl[8 + i];
             }
-            wave_lds_sync();
-            // x' = [R2 0..7, R1 1..7, R1 0], y' = [R1 0, R1 9..15, R2 8..15]; R1[8] (bin N/2) apart
-#pragma unroll
-            for (int i = 0; i < 8; ++i) R1[i] = csel(sp, spl[16 + i], R1[i]);
-#pragma unroll
-            for (int i = 8; i < 15; ++i) R1[i] = csel(sp, spl[i - 7], R1[i]);
-            R1[15] = csel(sp, spl[0], R1[15]);
-            R2[0] = csel(sp, spl[0], R2[0]);
-#pragma unroll
-            for (int i = 1; i < 8; ++i) R2[i] = csel(sp, spl[8 + i], R2[i]);
         }
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -640,24 +634,22 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
             __builtin_amdgcn_sched_barrier(0);
         }
         if (wu == 0) {
-            wave_lds_sync(); // the permutation's reads of spl above precede these stores
             if (sp) {
+                // back: R1 = [x 15, x 8..14, conj(c8 v8), y 1..7], R2 = [x 0..7, y 8..15]
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
                     spl[i] = R1[i];
                     spl[16 + i] = R2[i];
                 }
+                R1[0] = spl[15];
+#pragma unroll
+                for (int i = 1; i < 8; ++i) R1[i] = spl[7 + i];
+                R1[8] = make_double2(v8.x * c8, -v8.y * c8);
+#pragma unroll
+                for (int i = 9; i < 16; ++i) R1[i] = spl[16 + i - 8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) R2[i] = spl[i];
             }
-            wave_lds_sync();
-            // back: R1 = [x 15, x 8..14, conj(c8 v8), y 1..7], R2 = [x 0..7, y 8..15]
-            R1[0] = csel(sp, spl[15], R1[0]);
-#pragma unroll
-            for (int i = 1; i < 8; ++i) R1[i] = csel(sp, spl[7 + i], R1[i]);
-            R1[8] = csel(sp, make_double2(v8.x * c8, -v8.y * c8), R1[8]);
-#pragma unroll
-            for (int i = 9; i < 16; ++i) R1[i] = csel(sp, spl[16 + i - 8], R1[i]);
-#pragma unroll
-            for (int i = 0; i < 8; ++i) R2[i] = csel(sp, spl[i], R2[i]);
         }
         // ---- inverse stage 3: DFT16 over lambda -> gamma (on conj(V))
         dft16f(R1);
