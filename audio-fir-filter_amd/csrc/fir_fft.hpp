@@ -781,6 +781,12 @@ struct FftNrm {
 // the rescale to the next barrier 1 kept kNrmK float4 live across the final
 // phase: 256 VGPRs and scratch spills.)
 constexpr int kNrmK = 14;
+#ifndef LCFIR_NRM_K32
+#define LCFIR_NRM_K32 16
+#endif
+// fir_fft32r_kernel's halves: up to kNrmK32 blocks of 1 024 floats each, so a
+// 60-min stereo file (15 blocks per half at 4 001 taps) still fuses
+constexpr int kNrmK32 = LCFIR_NRM_K32;
 constexpr int kVmcntNrm = 0x0F70 | kNrmK; // s_waitcnt vmcnt(kNrmK): the slice's stores may stay in flight
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t fft_nrm_rsrc(const FftNrm &nrm, int u, bool active = true) {
     const int64_t s0 = (int64_t)u * nrm.slice;
@@ -791,17 +797,19 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t fft_nrm_rsrc(const FftNrm &nrm
 // unconditional for every wave (an inactive one loads through an empty
 // resource: no memory traffic), so v is defined on every path and never
 // live across the column phase
-__device__ __forceinline__ void fft_nrm_load(const FftNrm &nrm, int u, int t, bool active, float4 (&v)[kNrmK]) {
+template <int K = kNrmK>
+__device__ __forceinline__ void fft_nrm_load(const FftNrm &nrm, int u, int t, bool active, float4 (&v)[K]) {
     const __amdgpu_buffer_rsrc_t r = fft_nrm_rsrc(nrm, u, active);
 #pragma unroll
-    for (int k = 0; k < kNrmK; ++k)
+    for (int k = 0; k < K; ++k)
         v[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, 16 * t + 4096 * k, 0, kNtStore));
 }
-__device__ __forceinline__ void fft_nrm_store(const FftNrm &nrm, int u, int t, double gain, float4 (&v)[kNrmK]) {
+template <int K = kNrmK>
+__device__ __forceinline__ void fft_nrm_store(const FftNrm &nrm, int u, int t, double gain, float4 (&v)[K]) {
     const __amdgpu_buffer_rsrc_t r = fft_nrm_rsrc(nrm, u);
     using b128_t = decltype(__builtin_amdgcn_raw_buffer_load_b128(r, 0, 0, 0));
 #pragma unroll
-    for (int k = 0; k < kNrmK; ++k) {
+    for (int k = 0; k < K; ++k) {
         v[k].x = (float)((double)v[k].x * gain);
         v[k].y = (float)((double)v[k].y * gain);
         v[k].z = (float)((double)v[k].z * gain);
@@ -1614,7 +1622,8 @@ inline int64_t fft_chunk(const FftPlan &plan) {
 }
 
 // work array + twiddles + 8 f32 peak slots + the special lane's 32 double2
-constexpr size_t kR32LdsBytes = sizeof(double2) * (size_t)(kR32Work + kR32Tw + 2 + 32);
+// (+ 256 B that the L2 prefetch's LDS-DMA writes and nobody reads)
+constexpr size_t kR32LdsBytes = sizeof(double2) * (size_t)(kR32Work + kR32Tw + 2 + 32 + (LCFIR_R32_PF ? 16 : 0));
 
 template <int kOut, bool kNrm = false>
 inline bool fft32r_launch_one(const FftPlan &plan, const DirectParams &q, int nch, hipStream_t s, std::string &err,
@@ -1628,10 +1637,10 @@ inline bool fft32r_launch_one(const FftPlan &plan, const DirectParams &q, int nc
     const int64_t units = nseg * nch; // < 2^31 (fft_launch)
     const int64_t grid = std::min<int64_t>(units, (int64_t)plan.cus);
     if constexpr (kNrm) {
-        // whole 2 048-float blocks per unit (two halves of <= kNrmK x 1 024, fft_nrm_fusable)
+        // whole 2 048-float blocks per unit (two halves of <= kNrmK32 x 1 024, fft_nrm_fusable)
         const int64_t per = (nrm.count + units - 1) / units;
         nrm.slice = (per + 2047) / 2048 * 2048;
-        if (nrm.slice > (int64_t)kNrmK * 2048) {
+        if (nrm.slice > (int64_t)kNrmK32 * 2048) {
             err = "normalize slice too large to fuse";
             return false;
         }
@@ -1777,8 +1786,8 @@ inline bool fft_launch_group(const FftPlan &plan, const DirectParams &p, int nch
 // launch?  Single-partition filters on the L = 16 384 or the register-resident
 // L = 32 768 kernel, 16-B aligned buffer; otherwise the caller runs the
 // normalize pass itself.  The first launch (the one that carries it) must
-// spread the previous file's floats at <= kNrmK x 1 024 per unit (x 2 048 on
-// the register kernel: two halves).
+// spread the previous file's floats at <= kNrmK x 1 024 per unit (kNrmK32 x
+// 2 048 on the register kernel: two halves).
 inline bool fft_nrm_fusable(const FftPlan &plan, const FftNrm &nrm, const DirectParams &p, int nch) {
     if (plan.parts != 1 || (plan.L != kFftL && !plan.reg32) || !nrm.y || !nrm.peak || nrm.npeak < 1 ||
         (reinterpret_cast<uintptr_t>(nrm.y) & 15) != 0 || p.end <= p.start || nch <= 0)
@@ -1787,8 +1796,8 @@ inline bool fft_nrm_fusable(const FftPlan &plan, const FftNrm &nrm, const Direct
     const int64_t group = std::max<int64_t>(1, std::min<int64_t>(nch, fft_max_units(plan) / nseg));
     const int64_t units = nseg * group;
     const int64_t per = (nrm.count + units - 1) / units;
-    // fir_fft32r_kernel takes two halves of up to kNrmK x 1 024 floats per unit
-    return plan.reg32 ? (per + 2047) / 2048 <= kNrmK : (per + 1023) / 1024 <= kNrmK;
+    // fir_fft32r_kernel takes two halves of up to kNrmK32 x 1 024 floats per unit
+    return plan.reg32 ? (per + 2047) / 2048 <= kNrmK32 : (per + 1023) / 1024 <= kNrmK;
 }
 // nrm: a previous file's normalize to fuse (fft_nrm_fusable must hold), or null
 inline bool fft_launch(const FftPlan &plan, const DirectParams &p, int nch, hipStream_t s,

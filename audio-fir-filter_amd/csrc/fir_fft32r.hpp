@@ -48,6 +48,12 @@ constexpr int kR32TwG = 1024;   // W_512^g, g < 16
 constexpr int kR32Tw = 1024 + 16;
 constexpr size_t kR32PairTable = (size_t)24 * kFftNT; // double2: (p1, q2) [16][512], (p2 even, p2 odd) [8][512]
 constexpr int kR32SpecialLane = 31;                   // of wave 0
+#ifndef LCFIR_R32_STORE
+#define LCFIR_R32_STORE 1 // full units' outputs: 1 = quad stores (DPP pair trade), 2 = pair stores, rsrc range check
+#endif
+#ifndef LCFIR_R32_PF
+#define LCFIR_R32_PF 0 // 1: the older waves pull the next unit's samples into L2 at barrier 1 (LDS-DMA, dummy target)
+#endif
 #ifndef LCFIR_R32_PAD
 #define LCFIR_R32_PAD 1 // T2's rows padded to 17 slots: conflict-free without an XOR swizzle's address math (-5 %)
 #endif
@@ -340,6 +346,25 @@ __device__ __forceinline__ void r32_stage_samples(const DirectParams &p, int ch,
     }
 }
 
+// The next unit's samples into L2 while the older waves (threads t < 256)
+// wait at T1's first barrier, so the final phase's LDS-DMA of them (every CU
+// at once) hits L2 instead of queueing on HBM.  One dword per 64-B line,
+// through LDS-DMA into a 256-B area nobody reads (no VGPR destination, no
+// compiler-tracked load: the later vmcnt waits only over-count).  Edge units
+// (window before the channel start) are left to the DMA.
+__device__ __forceinline__ void r32_prefetch_samples(const DirectParams &p, int ch, int64_t n0, int t,
+                                                     fft_lds_void *dummy) {
+    const float *x = p.x + (int64_t)ch * p.x_stride;
+    const int64_t w0 = n0 - p.half - p.x_lo;
+    if (w0 < 0 || w0 >= p.x_hi - p.x_lo) return;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float *>(x), (short)0, (int)((p.x_hi - p.x_lo) * 4), 0x00020000);
+    const int sofs = (int)(w0 * 4);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) // 8 x 256 lines of 64 B = the unit's 128 KiB
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, dummy, 4, 64 * t, sofs + 16384 * i, 0, 0);
+}
+
 // Outputs of one unit: c[2m] = Re out[n], c[2m+1] = -Im out[n], m = j + 512 n,
 // valid for c in [half, L - half); sg = the sign bit waves 4..7 put on odd n
 // (their rotated final DFT32).  Range-checked buffer stores, nt, as
@@ -358,6 +383,32 @@ __device__ __forceinline__ float r32_store_unit(const DirectParams &p, int ch, i
         f0 = __int_as_float(__float_as_int((float)o[n].x) ^ s);
         f1 = __int_as_float(__float_as_int((float)(-o[n].y)) ^ s);
     };
+#if LCFIR_R32_STORE == 2
+    if ((cmin & 1) == 0 && n0 >= p.start && (p.end - n0 >= B || ((p.end - n0) & 1) == 0)) {
+        // pair stores: lane j's (c, c + 1) = 2 (j + 512 n) + {0, 1} as one 8-byte
+        // store through a resource over exactly the unit's valid outputs
+        // [n0, min(n0 + B, end)): the hardware range check drops the halo
+        // (c < cmin wraps to a huge offset, c >= cmax lands past the end) and
+        // the peak takes the lanes the same unsigned compare admits (whole
+        // pairs: cmin and the record count are even)
+        const int nrec = 4 * (int)(p.end - n0 < B ? p.end - n0 : B);
+        const __amdgpu_buffer_rsrc_t yu =
+            __builtin_amdgcn_make_buffer_rsrc(yb + (n0 - p.start), (short)0, nrec, 0x00020000);
+        const int v0 = 8 * j - 4 * cmin;
+        using b64_t = decltype(__builtin_amdgcn_raw_buffer_load_b64(yu, 0, 0, 0));
+#pragma unroll
+        for (int n = 0; n < 32; ++n) {
+            float f0, f1;
+            F(n, f0, f1);
+            const int vo = v0 + 4096 * n;
+            const float m = fmaxf(fabsf(f0), fabsf(f1));
+            pk = (unsigned)vo < (unsigned)nrec ? fmaxf(pk, m) : pk;
+            __builtin_amdgcn_raw_buffer_store_b64(
+                __builtin_bit_cast(b64_t, make_int2(__float_as_int(f0), __float_as_int(f1))), yu, vo, 0,
+                kFft32StoreAux);
+        }
+    } else
+#endif
     if ((cmin & 3) == 0 && n0 >= p.start && n0 + B <= p.end) {
         // quad stores: lanes j and j ^ 1 trade one pair (DPP quad_perm [1,0,3,2])
         const bool odd = j & 1;
@@ -443,9 +494,9 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
                 __builtin_amdgcn_s_setprio(0);
                 FftNrm nh = nrm;
                 nh.slice = nrm.slice / 2;
-                float4 nv[kNrmK];
-                fft_nrm_load(nh, 2 * u + h, j, true, nv);
-                fft_nrm_store(nh, 2 * u + h, j, nrm_gain, nv);
+                float4 nv[kNrmK32];
+                fft_nrm_load<kNrmK32>(nh, 2 * u + h, j, true, nv);
+                fft_nrm_store<kNrmK32>(nh, 2 * u + h, j, nrm_gain, nv);
                 __builtin_amdgcn_s_setprio(1);
             }
         }
@@ -511,6 +562,16 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
         for (int i = 0; i < 16; ++i) flds[kR32Rg * w + 64 * i + lane] = a[i];
         R32_STAMP(2);
         nrm_half(u, 0, j, wu);
+#if LCFIR_R32_PF
+        if (wu < 4) {
+            const int un1 = fft_unit32(rnd + 1, blockIdx.x, gridDim.x, gd.units);
+            if (un1 < gd.units) {
+                const int cn = fft_div(un1, gd);
+                r32_prefetch_samples(p, cn, p.seg0 + (int64_t)(un1 - cn * gd.nseg) * B, j,
+                                     (fft_lds_void *)(spl + 32));
+            }
+        }
+#endif
         r32_bar();
         R32_STAMP(3);
         if (pk_pending >= 0) {
@@ -633,6 +694,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
                          R2[15 - i]);
             __builtin_amdgcn_sched_barrier(0);
         }
+        R32_STAMP(12);
         if (wu == 0) {
             if (sp) {
                 // back: R1 = [x 15, x 8..14, conj(c8 v8), y 1..7], R2 = [x 0..7, y 8..15]

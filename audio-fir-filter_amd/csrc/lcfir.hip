@@ -64,6 +64,9 @@ struct lcfir_ctx {
     // the plan (lcfir_ctx_set_fft_tuning), and freed by lcfir_ctx_destroy
     bool plan_captured = false;
     std::vector<lcfir::FftPlan> retired_plans;
+    // previous-file normalizes (lcfir_filter_window_norm_dev): carried inside
+    // the filter launch / run as their own pass (lcfir_ctx_nrm_stats)
+    std::atomic<int64_t> nrm_fused{0}, nrm_separate{0};
 };
 
 namespace {
@@ -251,11 +254,13 @@ int run_filter(lcfir_ctx *ctx, lcfir::DirectParams p, int nch, hipStream_t s,
         const bool fuse = nrm && lcfir::fft_nrm_fusable(ctx->fft, *nrm, p, nch);
         if (!lcfir::fft_launch(ctx->fft, p, nch, s, err, fuse ? nrm : nullptr))
             return fail(LCFIR_EDEVICE, "fft launch: %s", err.c_str());
+        if (fuse) ++ctx->nrm_fused;
         if (!nrm || fuse) return LCFIR_OK;
     } else {
         const int rc = launch_direct(p, nch, s);
         if (rc || !nrm) return rc;
     }
+    ++ctx->nrm_separate;
     return launch_normalize(nrm->y, nrm->count, 1, nrm->count, nrm->peak, nrm->npeak, nrm->force, nullptr, 0, s);
 }
 
@@ -594,6 +599,13 @@ int lcfir_ctx_fft_info(lcfir_ctx *ctx, int32_t *seg_len, int32_t *parts, int32_t
     *seg_len = ctx->fft.L;
     *parts = ctx->fft.parts;
     *zero_phase = ctx->fft.sym ? 1 : 0;
+    return LCFIR_OK;
+}
+
+int lcfir_ctx_nrm_stats(const lcfir_ctx *ctx, int64_t *fused, int64_t *separate) {
+    if (!ctx || !fused || !separate) return fail(LCFIR_EINVAL, "null argument");
+    *fused = ctx->nrm_fused.load();
+    *separate = ctx->nrm_separate.load();
     return LCFIR_OK;
 }
 

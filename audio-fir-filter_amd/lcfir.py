@@ -68,6 +68,7 @@ _SIGNATURES = {
     "lcfir_ctx_half": ([_ctxp, ctypes.POINTER(_c_i32)], _c_int),
     "lcfir_ctx_fft_info": ([_ctxp, ctypes.POINTER(_c_i32), ctypes.POINTER(_c_i32), ctypes.POINTER(_c_i32)],
                            _c_int),
+    "lcfir_ctx_nrm_stats": ([_ctxp, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i64)], _c_int),
     "lcfir_ctx_set_fft_tuning": ([_ctxp, _c_i32, _c_i32, _c_i64, _c_i64], _c_int),
     "lcfir_ctx_ntaps": ([_ctxp, ctypes.POINTER(_c_i32)], _c_int),
     "lcfir_ctx_window": ([_ctxp, _c_i64, _c_i64, _c_i64, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i64)], _c_int),
@@ -221,6 +222,14 @@ class Filter:
         L, P, Z = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
         _check(load().lcfir_ctx_fft_info(self._ctx, ctypes.byref(L), ctypes.byref(P), ctypes.byref(Z)))
         return {"seg_len": L.value, "parts": P.value, "zero_phase": bool(Z.value)}
+
+    @property
+    def nrm_stats(self) -> dict:
+        """lcfir_ctx_nrm_stats: previous-file normalizes carried inside the
+        filter launch ("fused") and run as their own pass ("separate")."""
+        f, sep = ctypes.c_int64(), ctypes.c_int64()
+        _check(load().lcfir_ctx_nrm_stats(self._ctx, ctypes.byref(f), ctypes.byref(sep)))
+        return {"fused": f.value, "separate": sep.value}
 
     def set_fft_tuning(self, seg_len: int = 0, zero_phase: bool = True, chunk: int = 0, max_units: int = 0):
         """lcfir_ctx_set_fft_tuning: explicit FFT-method choices (tests run

@@ -5,7 +5,9 @@
 // phase of a steady-state unit over 64 workgroups.
 //   hipcc -O3 -std=c++2b --offload-arch=gfx950 -I../csrc -DLCFIR_FFT32R=1 -DLCFIR_FFT32R_TRACE \
 //         fft32r_trace.hip -o fft32r_trace
-//   ./fft32r_trace [ntaps] [seg_len]
+//   ./fft32r_trace [ntaps] [seg_len] [sym|asym] [nrm]
+// "nrm": every launch also carries a previous file's normalize (FftNrm) of
+// n x nch floats, as config 5's fused form does.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -101,7 +103,27 @@ int main(int argc, char **argv) {
         CK(hipMalloc(reinterpret_cast<void **>(&p.y64), nscr * sizeof(double)));
         p.y64_stride = std::min<int64_t>(p.end - p.start, lcfir::fft_chunk_span(plan));
     }
-    auto launch = [&]() { return lcfir::fft_launch(plan, p, nch, nullptr, err); };
+    const bool with_nrm = argc > 4 && std::string(argv[4]) == "nrm";
+    lcfir::FftNrm nrm{};
+    if (with_nrm) {
+        float *dprev;
+        unsigned *dnpk;
+        CK(hipMalloc(&dprev, sizeof(float) * hx.size()));
+        CK(hipMemcpy(dprev, hx.data(), sizeof(float) * hx.size(), hipMemcpyHostToDevice));
+        CK(hipMalloc(&dnpk, 4));
+        const float two = 2.0f; // peak > 1: the rescale runs
+        CK(hipMemcpy(dnpk, &two, 4, hipMemcpyHostToDevice));
+        nrm.y = dprev;
+        nrm.peak = dnpk;
+        nrm.count = (int64_t)hx.size();
+        nrm.npeak = 1;
+        if (!lcfir::fft_nrm_fusable(plan, nrm, p, nch)) {
+            std::fprintf(stderr, "normalize not fusable at this shape\n");
+            return 1;
+        }
+        std::printf("fused normalize of %lld floats per launch\n", (long long)nrm.count);
+    }
+    auto launch = [&]() { return lcfir::fft_launch(plan, p, nch, nullptr, err, with_nrm ? &nrm : nullptr); };
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));

@@ -624,6 +624,9 @@ def main():
                 "normalize": bool(args.normalize), "peak_scope": args.peak_scope,
                 "peak_exchange": runner.exchange,
                 "fused_normalize": runner.fuse and len(runner.shards) > 1,
+                # whole run (pre-roll included): normalizes carried inside a
+                # filter launch vs run as their own pass (lcfir_ctx_nrm_stats)
+                "normalize_launches": flt.nrm_stats if args.normalize else None,
                 "lanes": args.lanes,
                 "hip_graph": {"replays": n_replay, "steps_per_replay": graphed.per_replay,
                               "graphs": len(graphed.graphs), "eager_steps": n_eager} if graphed else None,

@@ -82,6 +82,10 @@ int lcfir_ctx_ntaps(const lcfir_ctx *ctx, int32_t *ntaps);
  * the filter runs in zero-phase form (linear-phase taps).  All 0 when the tap
  * count is outside the FFT method's range. */
 int lcfir_ctx_fft_info(lcfir_ctx *ctx, int32_t *seg_len, int32_t *parts, int32_t *zero_phase);
+/* Diagnostic: how many previous-file normalizes (lcfir_filter_window_norm_dev
+ * with ncount > 0) this ctx carried inside its filter launch (*fused) and how
+ * many it ran as their own pass (*separate) since it was created. */
+int lcfir_ctx_nrm_stats(const lcfir_ctx *ctx, int64_t *fused, int64_t *separate);
 /* Explicit FFT-method choices for this ctx (the library reads no environment
  * variables).  seg_len: 0 = automatic, or 16384 / 32768.  Automatic picks the
  * length with the lower estimated time per output for the taps alone: tap

@@ -216,6 +216,7 @@ def test_configs_4_and_5_batch(tt, oracle_mod):
         assert torch.equal(res4[f][1], res4[f % 2][1])
     del res4
 
+    s0 = flt.nrm_stats
     r5 = run(True)
     peaks5 = r5.peaks.cpu().numpy()
     assert np.array_equal(peaks5, peaks4)  # the per-file peak, pre-normalize
@@ -228,6 +229,10 @@ def test_configs_4_and_5_batch(tt, oracle_mod):
         else:
             # loud files: config 4 rescaled them already; --normalize gives the same
             assert torch.equal(y, r4.results()[sh.file][1])
+    # every file's normalize but the last rode in the next file's filter launch
+    # (a 60-min file's slice fits the fused form on both FFT kernels)
+    s1 = flt.nrm_stats
+    assert s1["fused"] - s0["fused"] >= nfiles - 1 and s1["separate"] == s0["separate"], (s0, s1)
     del r5
     # config 5's per-rank shape at N = 8: one file per rank with the peak
     # exchange in every step (force_exchange; the all-reduce is the identity at
@@ -239,9 +244,12 @@ def test_configs_4_and_5_batch(tt, oracle_mod):
                           force_exchange=True)
     assert r.defer
     r.prepare(lambda f, lo, hi: src[0][:, lo:hi])
+    s0 = flt.nrm_stats
     for _ in range(3):
         r.step()
     (sh, y), = r.results()
+    s1 = flt.nrm_stats
+    assert s1["fused"] - s0["fused"] >= 2 and s1["separate"] == s0["separate"], (s0, s1)
     assert float(r.peaks[0].item()) == peaks4[0]
     gain = 1.0 / float(np.float32(peaks4[0]))
     assert torch.equal(y, (pre[0].double() * gain).float())
