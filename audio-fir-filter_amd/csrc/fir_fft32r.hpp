@@ -49,11 +49,25 @@ constexpr int kR32Tw = 1024 + 16;
 constexpr size_t kR32PairTable = (size_t)24 * kFftNT; // double2: (p1, q2) [16][512], (p2 even, p2 odd) [8][512]
 constexpr int kR32SpecialLane = 31;                   // of wave 0
 #ifndef LCFIR_R32_STORE
-#define LCFIR_R32_STORE 1 // full units' outputs: 1 = quad stores (DPP pair trade), 2 = pair stores, rsrc range check
+#define LCFIR_R32_STORE 2 // full units' outputs: 1 = quad stores (DPP pair trade), 2 = pair stores, rsrc range check
 #endif
 #ifndef LCFIR_R32_PF
 #define LCFIR_R32_PF 0 // 1: the older waves pull the next unit's samples into L2 at barrier 1 (LDS-DMA, dummy target)
 #endif
+#ifndef LCFIR_R32_STAGGER
+#define LCFIR_R32_STAGGER 0 // experiment: odd workgroups start N x 8 128 cycles late (spreads the final phases' HBM bursts)
+#endif
+#ifndef LCFIR_R32_DMASPLIT
+#define LCFIR_R32_DMASPLIT 4 // 4: the next unit's LDS-DMA issued in quarters between the final phase's VALU blocks (0: at once)
+#endif
+#ifndef LCFIR_R32_DMA_AUX
+#define LCFIR_R32_DMA_AUX 0 // cache policy of the samples' LDS-DMA (2 = nt)
+#endif
+#ifndef LCFIR_R32_LATEWAIT
+#define LCFIR_R32_LATEWAIT 1 // 1 (needs LCFIR_R32_STORE 2): pair-path units store before the DMA wait, which moves to the next unit's top as vmcnt(32)
+#endif
+static_assert(!LCFIR_R32_LATEWAIT || (LCFIR_R32_STORE == 2 && LCFIR_R32_DMASPLIT == 4),
+              "the late DMA wait counts the pair path's 32 stores after the asm-issued split DMA");
 #ifndef LCFIR_R32_PAD
 #define LCFIR_R32_PAD 1 // T2's rows padded to 17 slots: conflict-free without an XOR swizzle's address math (-5 %)
 #endif
@@ -191,7 +205,9 @@ constexpr double kW32Rat[16] = {0.0, 0.19891236737965800691, 0.41421356237309504
 // forward 32-point DFT, natural order in and out: radix 2 over two DFT16s, each
 // butterfly's W32^k rotation in FMA form (the factor f folded into the
 // butterfly: 6 f64 operations per k instead of 8)
-__device__ __forceinline__ void dft32(double2 (&a)[32]) {
+// (hook: called between the two DFT16s)
+template <class Hook>
+__device__ __forceinline__ void dft32_hook(double2 (&a)[32], Hook &&hook) {
     double2 e[16], o[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -199,6 +215,7 @@ __device__ __forceinline__ void dft32(double2 (&a)[32]) {
         o[r] = a[2 * r + 1];
     }
     dft16f(e);
+    hook();
     dft16f(o);
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
@@ -218,6 +235,9 @@ __device__ __forceinline__ void dft32(double2 (&a)[32]) {
         a[k] = make_double2(__builtin_fma(fs, q.x, e[k].x), __builtin_fma(fs, q.y, e[k].y));
         a[k + 16] = make_double2(__builtin_fma(-fs, q.x, e[k].x), __builtin_fma(-fs, q.y, e[k].y));
     }
+}
+__device__ __forceinline__ void dft32(double2 (&a)[32]) {
+    dft32_hook(a, [] {});
 }
 
 // a[off + r] *= s0 w^r, r < 16, for a unit w: s_{r+2} = 2 Re(w^2) s_r - s_{r-2}
@@ -321,6 +341,49 @@ __device__ __forceinline__ void r32_chain_k1acc(double2 (&a)[32], double2 w, dou
 // has retired the wave's reads of its region).  Interior units by LDS-DMA
 // (16 b128 transfers per lane, no VGPRs); edge units through fft_load_unit's
 // range-checked loads.
+// interior unit of channel ch at n0: its window lies inside [x_lo, x_hi)
+__device__ __forceinline__ bool r32_interior(const DirectParams &p, int64_t n0) {
+    const int64_t w0 = n0 - p.half - p.x_lo;
+    return w0 >= 0 && w0 + kFft32L <= p.x_hi - p.x_lo;
+}
+// One LDS-DMA transfer (16 B per lane to LDS byte lds + 16 lane) issued by
+// inline asm: the compiler then does not know it writes LDS, so it adds no
+// vmcnt(0) before the next unit's LDS reads; LCFIR_R32_LATEWAIT's explicit
+// vmcnt(32) orders them instead (every later compiler wait only over-counts).
+__device__ __forceinline__ void r32_dma_asm(const float *base, uint32_t nbytes, uint32_t lds, int vofs, int sofs) {
+    typedef unsigned u4 __attribute__((ext_vector_type(4)));
+    const uint64_t a = reinterpret_cast<uint64_t>(base);
+    const u4 rs = {(unsigned)a, (unsigned)(a >> 32) & 0xFFFFu, nbytes, 0x00020000u};
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm" // m0 is reserved; the compiler sets it before each of its own uses
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds" ::"s"(lds), "v"(vofs), "s"(rs),
+                 "s"(sofs)
+                 : "memory", "m0");
+#pragma clang diagnostic pop
+}
+// transfers [s0, s1) of an interior unit's LDS-DMA (r32_stage_samples)
+template <int s0, int s1>
+__device__ __forceinline__ void r32_dma_part(const DirectParams &p, int ch, int64_t n0, int j, double2 *flds) {
+    const int w = j >> 6, lane = j & 63;
+    const float *x = p.x + (int64_t)ch * p.x_stride;
+    const int64_t w0 = n0 - p.half - p.x_lo;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float *>(x), (short)0, (int)((p.x_hi - p.x_lo) * 4), 0x00020000);
+    const int vofs = 4096 * (lane >> 5) + 512 * w + 16 * (lane & 31);
+    const int sofs = (int)(w0 * 4);
+#pragma unroll
+    for (int s = s0; s < s1; ++s) {
+#if LCFIR_R32_LATEWAIT
+        (void)rsrc;
+        r32_dma_asm(x, (uint32_t)((p.x_hi - p.x_lo) * 4),
+                    __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(fft_lds_void *)(flds + kR32Rg * w + 64 * s)),
+                    vofs, sofs + 8192 * s);
+#else
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (fft_lds_void *)(flds + kR32Rg * w + 64 * s), 16, vofs,
+                                                 sofs + 8192 * s, 0, LCFIR_R32_DMA_AUX);
+#endif
+    }
+}
 __device__ __forceinline__ void r32_stage_samples(const DirectParams &p, int ch, int64_t n0, int j, double2 *flds) {
     const int w = j >> 6, lane = j & 63;
     const float *x = p.x + (int64_t)ch * p.x_stride;
@@ -336,7 +399,7 @@ __device__ __forceinline__ void r32_stage_samples(const DirectParams &p, int ch,
 #pragma unroll
         for (int s = 0; s < 16; ++s)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (fft_lds_void *)(flds + kR32Rg * w + 64 * s), 16, vofs,
-                                                     sofs + 8192 * s, 0, 0);
+                                                     sofs + 8192 * s, 0, LCFIR_R32_DMA_AUX);
     } else {
         float2 v[32];
         fft_load_unit<32>(p, ch, n0, j, v);
@@ -365,6 +428,11 @@ __device__ __forceinline__ void r32_prefetch_samples(const DirectParams &p, int 
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, dummy, 4, 64 * t, sofs + 16384 * i, 0, 0);
 }
 
+// a unit whose outputs take the pair-store path (32 stores per lane)
+__device__ __forceinline__ bool r32_pair_path(const DirectParams &p, int64_t n0, int B) {
+    return (p.half & 1) == 0 && n0 >= p.start && (p.end - n0 >= B || ((p.end - n0) & 1) == 0);
+}
+
 // Outputs of one unit: c[2m] = Re out[n], c[2m+1] = -Im out[n], m = j + 512 n,
 // valid for c in [half, L - half); sg = the sign bit waves 4..7 put on odd n
 // (their rotated final DFT32).  Range-checked buffer stores, nt, as
@@ -384,7 +452,7 @@ __device__ __forceinline__ float r32_store_unit(const DirectParams &p, int ch, i
         f1 = __int_as_float(__float_as_int((float)(-o[n].y)) ^ s);
     };
 #if LCFIR_R32_STORE == 2
-    if ((cmin & 1) == 0 && n0 >= p.start && (p.end - n0 >= B || ((p.end - n0) & 1) == 0)) {
+    if (r32_pair_path(p, n0, B)) {
         // pair stores: lane j's (c, c + 1) = 2 (j + 512 n) + {0, 1} as one 8-byte
         // store through a resource over exactly the unit's valid outputs
         // [n0, min(n0 + B, end)): the hardware range check drops the halo
@@ -512,6 +580,8 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
     }
     __builtin_amdgcn_s_waitcnt(kVmcnt0);
     __syncthreads();
+    if (LCFIR_R32_STAGGER > 0 && (blockIdx.x & 1))
+        for (int i = 0; i < LCFIR_R32_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
     uint32_t tk_all = task[threadIdx.x];
     asm volatile("" : "+v"(tk_all));
     float pk_run = 0.0f;
@@ -528,6 +598,11 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
         const int ch = fft_div(u, gd);
         const int64_t n0 = p.seg0 + (int64_t)(u - ch * gd.nseg) * B;
         double2 a[32];
+#if LCFIR_R32_LATEWAIT
+        // the staging transfers have landed; the previous unit's 32 pair
+        // stores (issued after them) may still be in flight
+        __builtin_amdgcn_s_waitcnt(0x8F70);
+#endif
         R32_STAMP(0);
         // ---- stage 1: the samples out of the wave's region (staged by the
         // previous unit), waves 4..7 negating the odd ones; DFT32; W_16384^(b k1)
@@ -789,22 +864,56 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
             const int un1 = fft_unit32(rnd + 1, blockIdx.x, gridDim.x, gd.units);
             const int un = un1 < gd.units ? un1 : u;
             const int cn = fft_div(un, gd);
-            r32_stage_samples(p, cn, p.seg0 + (int64_t)(un - cn * gd.nseg) * B, j, flds);
-        }
-        R32_STAMP(22);
-        // ---- final: * W_16384^(b k1), DFT32 over k1 -> n
-        {
+            const int64_t nn = p.seg0 + (int64_t)(un - cn * gd.nseg) * B;
+#if LCFIR_R32_DMASPLIT
+            const bool split = r32_interior(p, nn);
+            if (!split) r32_stage_samples(p, cn, nn, j, flds);
+#else
+            constexpr bool split = false;
+#ifndef LCFIR_R32_NODMA // timing-only diagnostic (wrong outputs): the next unit reuses stale LDS
+            r32_stage_samples(p, cn, nn, j, flds);
+#endif
+#endif
+            R32_STAMP(22);
+            // ---- final: * W_16384^(b k1), DFT32 over k1 -> n (an interior next
+            // unit's DMA issued in quarters between the VALU blocks, so a wave
+            // whose transfer waits for the CU's memory queue still computes)
+            auto part = [&](auto q) {
+                constexpr int k = decltype(q)::value;
+                if (split) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    r32_dma_part<4 * k, 4 * k + 4>(p, cn, nn, j, flds);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            };
             const double2 wb = twl[kR32TwB + j], w16 = twl[kR32TwB16 + j], one = make_double2(1.0, 0.0);
+            part(std::integral_constant<int, 0>{});
             if (LCFIR_R32_TW) {
-                r32_chain_k1acc(a, wb, w16, hi);
+                const double2 w2 = cmul(wb, wb);
+                const double2 w4 = cmul(w2, w2);
+                r32_chain_anchored<16>(a, 0, csel(hi, w16, one), wb, w4);
+                part(std::integral_constant<int, 1>{});
+                r32_chain_anchored<16>(a, 16, csel(hi, one, w16), wb, w4);
             } else {
                 r32_chain16(a, 0, csel(hi, w16, one), wb);
+                part(std::integral_constant<int, 1>{});
                 r32_chain16(a, 16, csel(hi, one, w16), wb);
             }
+            part(std::integral_constant<int, 2>{});
+            dft32_hook(a, [&] { part(std::integral_constant<int, 3>{}); });
         }
-        dft32(a);
+#if LCFIR_R32_LATEWAIT
+        // pair-path units: the DMA wait moves to the next unit's top
+        if (!r32_pair_path(p, n0, B)) __builtin_amdgcn_s_waitcnt(kVmcnt0);
+#else
         __builtin_amdgcn_s_waitcnt(kVmcnt0); // the staging transfers have landed (stage 1 reads them)
+#endif
+#ifdef LCFIR_R32_NOSTORE // timing-only diagnostic (wrong outputs): no output stores
+        float pk = 0.0f;
+        if (p.start < 0) pk = r32_store_unit(p, ch, n0, B, j, a, hi ? (int)0x80000000 : 0);
+#else
         const float pk = r32_store_unit(p, ch, n0, B, j, a, hi ? (int)0x80000000 : 0);
+#endif
         if (ch != pk_ch) {
             if (p.peak && pk_ch >= 0) {
                 fft_peak_stage(pk_lds, pk_run);
