@@ -68,6 +68,9 @@ constexpr int kR32SpecialLane = 31;                   // of wave 0
 #endif
 static_assert(!LCFIR_R32_LATEWAIT || (LCFIR_R32_STORE == 2 && LCFIR_R32_DMASPLIT == 4),
               "the late DMA wait counts the pair path's 32 stores after the asm-issued split DMA");
+#ifndef LCFIR_R32_PAIRLOAD
+#define LCFIR_R32_PAIRLOAD 0 // 1: the pair table's first half is loaded between stage 2's DFT16s
+#endif
 #ifndef LCFIR_R32_PAD
 #define LCFIR_R32_PAD 1 // T2's rows padded to 17 slots: conflict-free without an XOR swizzle's address math (-5 %)
 #endif
@@ -684,7 +687,22 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
         }
         R32_STAMP(7);
         // ---- stage 2: DFT32 over beta (rotated by 16 h), * (s W_512^gam)^kappa, s = (-1)^h
+        double2 pq[16], p2v[8];
+#if LCFIR_R32_PAIRLOAD
+        // the pair table's first half, issued between the DFT32's halves so a
+        // wave whose loads queue behind the CU's other transfers still computes
+        dft32_hook(c, [&] {
+            const double2 *pt = pair + j;
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) pq[i] = pt[512 * i];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) p2v[m] = pt[512 * (16 + m)];
+            __builtin_amdgcn_sched_barrier(0);
+        });
+#else
         dft32(c);
+#endif
         double2 wg = twl[kR32TwG + gam];
         if (h) wg = make_double2(-wg.x, -wg.y);
         if (LCFIR_R32_TW)
@@ -692,8 +710,8 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
         else
             r32_chain32(c, wg);
         R32_STAMP(8);
+#if !LCFIR_R32_PAIRLOAD
         // ---- the pair table's first half, in flight across T2
-        double2 pq[16], p2v[8];
         {
             const double2 *pt = pair + j;
 #pragma unroll
@@ -701,6 +719,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
 #pragma unroll
             for (int m = 0; m < 4; ++m) p2v[m] = pt[512 * (16 + m)];
         }
+#endif
         __builtin_amdgcn_sched_barrier(0);
         R32_STAMP(9);
         // ---- T2: two wave-local rounds (kappa < 16, kappa >= 16) in the wave's region
