@@ -788,6 +788,10 @@ constexpr int kNrmK = 14;
 // fir_fft32r_kernel's halves: up to kNrmK32 blocks of 1 024 floats each, so a
 // 60-min stereo file (15 blocks per half at 4 001 taps) still fuses
 constexpr int kNrmK32 = LCFIR_NRM_K32;
+#ifndef LCFIR_NRM_LOAD_AUX
+#define LCFIR_NRM_LOAD_AUX LCFIR_FFT_STORE_AUX // the slice's loads: nt, as its stores
+#endif
+constexpr int kNrmLoadAux = LCFIR_NRM_LOAD_AUX;
 constexpr int kVmcntNrm = 0x0F70 | kNrmK; // s_waitcnt vmcnt(kNrmK): the slice's stores may stay in flight
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t fft_nrm_rsrc(const FftNrm &nrm, int u, bool active = true) {
     const int64_t s0 = (int64_t)u * nrm.slice;
@@ -803,7 +807,7 @@ __device__ __forceinline__ void fft_nrm_load(const FftNrm &nrm, int u, int t, bo
     const __amdgpu_buffer_rsrc_t r = fft_nrm_rsrc(nrm, u, active);
 #pragma unroll
     for (int k = 0; k < K; ++k)
-        v[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, 16 * t + 4096 * k, 0, kNtStore));
+        v[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, 16 * t + 4096 * k, 0, kNrmLoadAux));
 }
 template <int K = kNrmK>
 __device__ __forceinline__ void fft_nrm_store(const FftNrm &nrm, int u, int t, double gain, float4 (&v)[K]) {
