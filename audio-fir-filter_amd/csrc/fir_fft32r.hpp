@@ -72,7 +72,7 @@ static_assert(!LCFIR_R32_LATEWAIT || (LCFIR_R32_STORE == 2 && LCFIR_R32_DMASPLIT
 #define LCFIR_R32_PAIRLOAD 0 // 1: the pair table's first half is loaded between stage 2's DFT16s
 #endif
 #ifndef LCFIR_R32_PAIR2
-#define LCFIR_R32_PAIR2 0 // 1: the pair table's second half loaded entry by entry as the first half's pairs retire
+#define LCFIR_R32_PAIR2 1 // 1: the pair table's second half loaded entry by entry as the first half's pairs retire
 #endif
 #ifndef LCFIR_R32_PAD
 #define LCFIR_R32_PAD 1 // T2's rows padded to 17 slots: conflict-free without an XOR swizzle's address math (-5 %)
@@ -552,6 +552,9 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
                                                            const uint32_t *__restrict__ task, int B, FftGrid gd,
                                                            double c8, FftNrm nrm) {
     extern __shared__ double2 flds[];
+    // the pair table's second half entry by entry (-2 %); the fused-rescale
+    // kernel keeps the block load (the early loads spill 6 more VGPRs there)
+    constexpr bool kPair2 = LCFIR_R32_PAIR2 && !kNrm;
     bool nrm_on = false;
     double nrm_gain = 1.0;
     if constexpr (kNrm) {
@@ -775,16 +778,15 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
         for (int i = 0; i < 8; ++i) {
             fft_pair_sym(R1[i], R2[15 - i], pq[i].x, pq[i].y, (i & 1) ? p2v[i >> 1].y : p2v[i >> 1].x, R1[i],
                          R2[15 - i]);
-#if LCFIR_R32_PAIR2
-            // the second half's entry 8 + i into the registers pair i has
-            // just freed, so each load has the remaining pairs to land in
-            pq[8 + i] = pair[j + 512 * (8 + i)];
-            if (i & 1) p2v[4 + (i >> 1)] = pair[j + 512 * (20 + (i >> 1))];
-#endif
+            if constexpr (kPair2) {
+                // the second half's entry 8 + i into the registers pair i has
+                // just freed, so each load has the remaining pairs to land in
+                pq[8 + i] = pair[j + 512 * (8 + i)];
+                if (i & 1) p2v[4 + (i >> 1)] = pair[j + 512 * (20 + (i >> 1))];
+            }
             __builtin_amdgcn_sched_barrier(0);
         }
-#if !LCFIR_R32_PAIR2
-        {
+        if constexpr (!kPair2) {
             // the second half of the table (its registers were the first half's)
             const double2 *pt = pair + j;
 #pragma unroll
@@ -792,7 +794,6 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
 #pragma unroll
             for (int m = 4; m < 8; ++m) p2v[m] = pt[512 * (16 + m)];
         }
-#endif
 #pragma unroll
         for (int i = 8; i < 16; ++i) {
             fft_pair_sym(R1[i], R2[15 - i], pq[i].x, pq[i].y, (i & 1) ? p2v[i >> 1].y : p2v[i >> 1].x, R1[i],
