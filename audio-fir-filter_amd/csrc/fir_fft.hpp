@@ -102,10 +102,7 @@ constexpr int kVmcnt0 = 0x0F70;     // s_waitcnt vmcnt(0) (expcnt, lgkmcnt left 
 // written once and every workgroup stores its segment in the same phase; nt
 // stores drain that burst faster (+5 % on config 2; nt, sc0 or sc1 on the
 // sample loads measured 0 to -5 %, so those stay cached)
-#ifndef LCFIR_FFT_STORE_AUX
-#define LCFIR_FFT_STORE_AUX 2
-#endif
-constexpr int kNtStore = LCFIR_FFT_STORE_AUX;
+constexpr int kNtStore = 2;
 // output modes of fir_fft_f64_kernel (see there)
 constexpr int kFftOutF32 = 0, kFftOutFirst = 1, kFftOutAdd = 2, kFftOutLast = 3, kFftOutSym = 4;
 // kFftOutSym = kFftOutF32 for a linear-phase filter in zero-phase form: real
@@ -209,20 +206,14 @@ inline int fft_partition_count(int ntaps, int L = 16384) {
 // the merge and the park slab, the general pair table and partitions cost
 // more there (register pressure).
 // Zero-phase single-partition L = 32768 plans run fir_fft32r_kernel (the
-// transform held in registers) unless a tools build turns it off; its unit
-// costs 2.2 L = 16 384 units (configs 2 and 3: 23.6 us against 10.7 us per
+// transform held in registers); its unit costs 2.2 L = 16 384 units (configs 2 and 3: 23.6 us against 10.7 us per
 // persistent-grid round), so it takes linear-phase filters
 // from ~4 000 taps (config 2's 4 001: 7.65e-5 against 8.07e-5 per output).
-#ifndef LCFIR_FFT32R
-#define LCFIR_FFT32R 1
-#endif
-#ifndef LCFIR_FFT32R_COST
-#define LCFIR_FFT32R_COST 2.2
-#endif
-inline bool fft_reg32(int L, int parts, bool sym) { return LCFIR_FFT32R && L == 32768 && parts == 1 && sym; }
+constexpr double kFft32rUnitCost = 2.2;
+inline bool fft_reg32(int L, int parts, bool sym) { return L == 32768 && parts == 1 && sym; }
 inline double fft_unit_cost(int L, int parts, bool sym) {
     if (L == 16384) return parts == 1 ? 1.0 : 1.25;
-    if (fft_reg32(L, parts, sym)) return LCFIR_FFT32R_COST;
+    if (fft_reg32(L, parts, sym)) return kFft32rUnitCost;
     return parts == 1 ? (sym ? 2.9 : 3.1) : 4.0;
 }
 // Estimated time per output with segment length L: partitions x unit cost /
@@ -409,9 +400,6 @@ __device__ __forceinline__ void dft4_r2(double2 &a0, double2 &a1, double2 u2, do
     a3 = csub(t1, t3);
 }
 
-#ifndef LCFIR_FFT_DFT16F
-#define LCFIR_FFT_DFT16F 0
-#endif
 constexpr double kT1 = 0.41421356237309504880; // tan(pi/8)
 // W16^1, W16^3 and W16^9 are cos(pi/8) times (1 - i tan), -i (1 + i tan) and
 // -(1 - i tan): the rotations by tan are two FMAs each (no MUL) and the common
@@ -443,28 +431,6 @@ __device__ __forceinline__ void dft16(double2 (&a)[16]) {
     // radix-4 over n1 for each n2: slot 4*n1 + n2 -> slot 4*k1 + n2
 #pragma unroll
     for (int n2 = 0; n2 < 4; ++n2) dft4(a[n2], a[4 + n2], a[8 + n2], a[12 + n2]);
-#if LCFIR_FFT_DFT16F
-    a[10] = w16<4>(a[10]);
-    dft4(a[0], a[1], a[2], a[3]);
-    {
-        double2 o1, o3; // row 1: (a4, kC1 rot16_1(a5), kR2 rot8_1(a6), kC1 rot16_3(a7))
-        dft4_r2c(a[4], rot16_1(a[5]), rot8_1(a[6]), a[6], rot16_3(a[7]), o1, o3);
-        a[5] = o1;
-        a[7] = o3;
-    }
-    {
-        double2 o1, o3; // row 2: (a8, kR2 rot8_1(a9), -i a10, kR2 rot8_3(a11))
-        dft4_r13(a[8], rot8_1(a[9]), a[10], rot8_3(a[11]), o1, o3);
-        a[9] = o1;
-        a[11] = o3;
-    }
-    {
-        double2 o1, o3; // row 3: (a12, kC1 rot16_3(a13), kR2 rot8_3(a14), kC1 rot16_9(a15))
-        dft4_r2c(a[12], rot16_3(a[13]), rot8_3(a[14]), a[14], rot16_9(a[15]), o1, o3);
-        a[13] = o1;
-        a[15] = o3;
-    }
-#else
     // twiddles W16^(n2*k1), slot 4*k1 + n2, then radix-4 over n2 for each k1:
     // slot 4*k1 + k2 holds X[k1 + 4*k2].  The W16^2 = W8^1 and W16^6 = W8^3
     // rotations keep their sqrt(1/2) pending into the radix-4 (dft4_r13 and
@@ -484,7 +450,6 @@ __device__ __forceinline__ void dft16(double2 (&a)[16]) {
         a[11] = o3;
     }
     dft4_r2(a[12], a[13], rot8_3(a[14]), a[14], a[15]); // row 3: (a12, a13 w3, kR2 rot8_3(a14), a15 w9)
-#endif
     double2 t[16];
 #pragma unroll
     for (int k1 = 0; k1 < 4; ++k1)
@@ -534,25 +499,6 @@ __device__ __forceinline__ void twiddle16(double2 (&a)[16], double2 w1) {
     a[15] = cmul(a[15], cmul(wo, w2));
 }
 
-#ifndef LCFIR_FFT_CHEB
-#define LCFIR_FFT_CHEB 0
-#endif
-#if LCFIR_FFT_CHEB
-// w[r] = w1^r for a unit w1, r = 1..15, by the Chebyshev recurrence
-// w^(r+2) = 2 Re(w^2) w^r - w^(r-2): two FMAs per power instead of a complex
-// multiply's two MULs and two FMAs; odd and even powers in two chains of depth 7
-__device__ __forceinline__ void powers16(double2 w1, double2 (&w)[16]) {
-    const double c2 = w1.x + w1.x;
-    w[1] = w1;
-    w[2] = make_double2(__builtin_fma(c2, w1.x, -1.0), c2 * w1.y);
-    const double q2 = w[2].x + w[2].x;
-    w[3] = make_double2(__builtin_fma(c2, w[2].x, -w1.x), __builtin_fma(c2, w[2].y, -w1.y));
-    w[4] = make_double2(__builtin_fma(q2, w[2].x, -1.0), q2 * w[2].y);
-#pragma unroll
-    for (int r = 5; r < 16; ++r)
-        w[r] = make_double2(__builtin_fma(q2, w[r - 2].x, -w[r - 4].x), __builtin_fma(q2, w[r - 2].y, -w[r - 4].y));
-}
-#else
 // w[r] = w1^r, r = 1..15, by twiddle16's chain (the same values, bit for bit)
 __device__ __forceinline__ void powers16(double2 w1, double2 (&w)[16]) {
     const double2 w2 = cmul(w1, w1);
@@ -565,27 +511,12 @@ __device__ __forceinline__ void powers16(double2 w1, double2 (&w)[16]) {
     }
     w[15] = cmul(w[13], w2);
 }
-#endif
 
 __device__ __forceinline__ void apply16(double2 (&a)[16], const double2 (&w)[16]) {
 #pragma unroll
     for (int r = 1; r < 16; ++r) a[r] = cmul(a[r], w[r]);
 }
 
-#if LCFIR_FFT_CHEB
-// w[r] = w1^r, r = 1..7 (powers16's recurrence, depth 4)
-__device__ __forceinline__ void powers8(double2 w1, double2 (&w)[8]) {
-    const double c2 = w1.x + w1.x;
-    w[1] = w1;
-    w[2] = make_double2(__builtin_fma(c2, w1.x, -1.0), c2 * w1.y);
-    const double q2 = w[2].x + w[2].x;
-    w[3] = make_double2(__builtin_fma(c2, w[2].x, -w1.x), __builtin_fma(c2, w[2].y, -w1.y));
-    w[4] = make_double2(__builtin_fma(q2, w[2].x, -1.0), q2 * w[2].y);
-#pragma unroll
-    for (int r = 5; r < 8; ++r)
-        w[r] = make_double2(__builtin_fma(q2, w[r - 2].x, -w[r - 4].x), __builtin_fma(q2, w[r - 2].y, -w[r - 4].y));
-}
-#else
 // w[r] = w1^r, r = 1..7 (depth <= 3)
 __device__ __forceinline__ void powers8(double2 w1, double2 (&w)[8]) {
     w[1] = w1;
@@ -596,7 +527,6 @@ __device__ __forceinline__ void powers8(double2 w1, double2 (&w)[8]) {
     w[6] = cmul(w[4], w[2]);
     w[7] = cmul(w[4], w[3]);
 }
-#endif
 
 __device__ __forceinline__ void twiddle8(double2 (&a)[8], const double2 (&w)[8]) {
 #pragma unroll
@@ -782,16 +712,10 @@ struct FftNrm {
 // the rescale to the next barrier 1 kept kNrmK float4 live across the final
 // phase: 256 VGPRs and scratch spills.)
 constexpr int kNrmK = 14;
-#ifndef LCFIR_NRM_K32
-#define LCFIR_NRM_K32 16
-#endif
 // fir_fft32r_kernel's halves: up to kNrmK32 blocks of 1 024 floats each, so a
 // 60-min stereo file (15 blocks per half at 4 001 taps) still fuses
-constexpr int kNrmK32 = LCFIR_NRM_K32;
-#ifndef LCFIR_NRM_LOAD_AUX
-#define LCFIR_NRM_LOAD_AUX LCFIR_FFT_STORE_AUX // the slice's loads: nt, as its stores
-#endif
-constexpr int kNrmLoadAux = LCFIR_NRM_LOAD_AUX;
+constexpr int kNrmK32 = 16;
+constexpr int kNrmLoadAux = kNtStore; // the slice's loads: nt, as its stores
 constexpr int kVmcntNrm = 0x0F70 | kNrmK; // s_waitcnt vmcnt(kNrmK): the slice's stores may stay in flight
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t fft_nrm_rsrc(const FftNrm &nrm, int u, bool active = true) {
     const int64_t s0 = (int64_t)u * nrm.slice;
@@ -1239,11 +1163,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
             const int c = 2 * (j + 512 * r);
             const float f0 = (float)a[r].x, f1 = (float)(-a[r].y);
             const bool ok = c >= cmin && (!kSym || c < cmax);
-#ifdef LCFIR_FFT_NOSTORE // timing-only tools builds: every store dropped by the range check
-            const int ob = (int)0x80000000;
-#else
             const int ob = ok ? (int)((off + c) * 4) : (int)0x80000000;
-#endif
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(f0), ys, ob, 0, kNtStore);
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(f1), ys, ob + 4, 0, kNtStore);
             pk = fmaxf(pk, ok ? fmaxf(fabsf(f0), fabsf(f1)) : 0.0f);
@@ -1627,14 +1547,14 @@ inline int64_t fft_chunk(const FftPlan &plan) {
 }
 
 // work array + twiddles + 8 f32 peak slots + the special lane's 32 double2
-// (+ 256 B that the L2 prefetch's LDS-DMA writes and nobody reads)
-constexpr size_t kR32LdsBytes = sizeof(double2) * (size_t)(kR32Work + kR32Tw + 2 + 32 + (LCFIR_R32_PF ? 16 : 0));
+constexpr size_t kR32LdsBytes = sizeof(double2) * (size_t)(kR32Work + kR32Tw + 2 + 32);
 
-template <int kOut, bool kNrm = false>
+// Probe: fir_fft32r_kernel's phase hook (tools/fft32r_trace.hip passes its own)
+template <int kOut, bool kNrm = false, class Probe = R32NoProbe>
 inline bool fft32r_launch_one(const FftPlan &plan, const DirectParams &q, int nch, hipStream_t s, std::string &err,
                               FftNrm nrm = FftNrm{}) {
     static const bool attr = [] {
-        return hipFuncSetAttribute(reinterpret_cast<const void *>(&fir_fft32r_kernel<kOut, kNrm>),
+        return hipFuncSetAttribute(reinterpret_cast<const void *>(&fir_fft32r_kernel<kOut, kNrm, Probe>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kR32LdsBytes) == hipSuccess;
     }();
     (void)attr;
@@ -1650,7 +1570,7 @@ inline bool fft32r_launch_one(const FftPlan &plan, const DirectParams &q, int nc
             return false;
         }
     }
-    hipLaunchKernelGGL((fir_fft32r_kernel<kOut, kNrm>), dim3((unsigned)grid), dim3(kFftNT), kR32LdsBytes, s, q,
+    hipLaunchKernelGGL((fir_fft32r_kernel<kOut, kNrm, Probe>), dim3((unsigned)grid), dim3(kFftNT), kR32LdsBytes, s, q,
                        plan.d_pair, plan.d_tw, plan.d_task, plan.B, fft_grid(nseg, units), plan.c8[0].x, nrm);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
@@ -1793,16 +1713,28 @@ inline bool fft_launch_group(const FftPlan &plan, const DirectParams &p, int nch
 // normalize pass itself.  The first launch (the one that carries it) must
 // spread the previous file's floats at <= kNrmK x 1 024 per unit (kNrmK32 x
 // 2 048 on the register kernel: two halves).
+// Floats of a previous file one unit of the plan's kernel rescales at most
+// (0: the kernel carries none): kNrmK blocks of 1 024 on the L = 16 384
+// kernel, two halves of kNrmK32 blocks on the register kernel.  Exported as
+// lcfir_ctx_fft_units' nrm_floats (tests size the fused / separate switch
+// from it).
+inline int64_t fft_nrm_unit_floats(const FftPlan &plan) {
+    if (plan.parts != 1) return 0;
+    if (plan.reg32) return (int64_t)kNrmK32 * 2048;
+    return plan.L == kFftL ? (int64_t)kNrmK * 1024 : 0;
+}
 inline bool fft_nrm_fusable(const FftPlan &plan, const FftNrm &nrm, const DirectParams &p, int nch) {
-    if (plan.parts != 1 || (plan.L != kFftL && !plan.reg32) || !nrm.y || !nrm.peak || nrm.npeak < 1 ||
-        (reinterpret_cast<uintptr_t>(nrm.y) & 15) != 0 || p.end <= p.start || nch <= 0)
+    const int64_t cap = fft_nrm_unit_floats(plan);
+    if (cap == 0 || !nrm.y || !nrm.peak || nrm.npeak < 1 || (reinterpret_cast<uintptr_t>(nrm.y) & 15) != 0 ||
+        p.end <= p.start || nch <= 0)
         return false;
     const int64_t nseg = fft_first_nseg(plan, p);
     const int64_t group = std::max<int64_t>(1, std::min<int64_t>(nch, fft_max_units(plan) / nseg));
     const int64_t units = nseg * group;
     const int64_t per = (nrm.count + units - 1) / units;
-    // fir_fft32r_kernel takes two halves of up to kNrmK32 x 1 024 floats per unit
-    return plan.reg32 ? (per + 2047) / 2048 <= kNrmK32 : (per + 1023) / 1024 <= kNrmK;
+    // whole blocks per unit: 2 048 floats on the register kernel (two halves), 1 024 otherwise
+    const int64_t blk = plan.reg32 ? 2048 : 1024;
+    return (per + blk - 1) / blk * blk <= cap;
 }
 // nrm: a previous file's normalize to fuse (fft_nrm_fusable must hold), or null
 inline bool fft_launch(const FftPlan &plan, const DirectParams &p, int nch, hipStream_t s,

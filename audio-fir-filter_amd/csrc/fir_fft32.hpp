@@ -78,15 +78,9 @@ __device__ unsigned long long g_fft32_trace[64][8][16];
 
 constexpr int kFft32L = 32768;
 // parked values per thread kept in registers (the rest in DirectParams::park)
-#ifndef LCFIR_FFT32_PARK_REGS
-#define LCFIR_FFT32_PARK_REGS 0 // tools builds try other values
-#endif
-constexpr int kParkRegs = LCFIR_FFT32_PARK_REGS;
+constexpr int kParkRegs = 0;
 constexpr int kParkSlab = 16 - kParkRegs; // double2 per thread in the slab
-#ifndef LCFIR_FFT32_STORE_AUX
-#define LCFIR_FFT32_STORE_AUX kNtStore // output store cache policy (tools builds try others)
-#endif
-constexpr int kFft32StoreAux = LCFIR_FFT32_STORE_AUX;
+constexpr int kFft32StoreAux = kNtStore; // output store cache policy
 // LDS twiddles: W_8192^i (i < 512), W_512^i (i < 64, fft_columns), W_16384^i (i < 512)
 constexpr int kFft32Tw = 512 + 64 + 512;
 constexpr int kFft32TwOdd = 576;
@@ -178,12 +172,8 @@ __device__ __forceinline__ float fft32_store_unit(const DirectParams &p, int ch,
                 q.w = odd ? __float_as_int(b1) : r1;
                 const int cq = 2 * (jq + 512 * (2 * k + (odd ? 1 : 0)));
                 const bool okq = cq >= cmin && (!kSym || cq < cmax);
-#ifdef LCFIR_FFT32_NOSTORE // timing-only builds: every store dropped by the range check
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(b128_t, q), ys, (int)0x80000000, 0, kFft32StoreAux);
-#else
                 __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(b128_t, q), ys,
                                                        okq ? (int)((off + cq) * 4) : (int)0x80000000, 0, kFft32StoreAux);
-#endif
             }
         } else if (n0 >= p.start && n0 + B <= p.end) {
             // every output of the unit is in [start, end); cmin is not a

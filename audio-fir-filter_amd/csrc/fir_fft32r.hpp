@@ -48,66 +48,40 @@ constexpr int kR32TwG = 1024;   // W_512^g, g < 16
 constexpr int kR32Tw = 1024 + 16;
 constexpr size_t kR32PairTable = (size_t)24 * kFftNT; // double2: (p1, q2) [16][512], (p2 even, p2 odd) [8][512]
 constexpr int kR32SpecialLane = 31;                   // of wave 0
-#ifndef LCFIR_R32_STORE
-#define LCFIR_R32_STORE 2 // full units' outputs: 1 = quad stores (DPP pair trade), 2 = pair stores, rsrc range check
-#endif
-#ifndef LCFIR_R32_PF
-#define LCFIR_R32_PF 0 // 1: the older waves pull the next unit's samples into L2 at barrier 1 (LDS-DMA, dummy target)
-#endif
-#ifndef LCFIR_R32_STAGGER
-#define LCFIR_R32_STAGGER 0 // experiment: odd workgroups start N x 8 128 cycles late (spreads the final phases' HBM bursts)
-#endif
-#ifndef LCFIR_R32_DMASPLIT
-#define LCFIR_R32_DMASPLIT 4 // 4: the next unit's LDS-DMA issued in quarters between the final phase's VALU blocks (0: at once)
-#endif
-#ifndef LCFIR_R32_DMA_AUX
-#define LCFIR_R32_DMA_AUX 0 // cache policy of the samples' LDS-DMA (2 = nt)
-#endif
-#ifndef LCFIR_R32_LATEWAIT
-#define LCFIR_R32_LATEWAIT 1 // 1 (needs LCFIR_R32_STORE 2): pair-path units store before the DMA wait, which moves to the next unit's top as vmcnt(32)
-#endif
-static_assert(!LCFIR_R32_LATEWAIT || (LCFIR_R32_STORE == 2 && LCFIR_R32_DMASPLIT == 4),
-              "the late DMA wait counts the pair path's 32 stores after the asm-issued split DMA");
-#ifndef LCFIR_R32_PAIRLOAD
-#define LCFIR_R32_PAIRLOAD 0 // 1: the pair table's first half is loaded between stage 2's DFT16s
-#endif
-#ifndef LCFIR_R32_PAIR2
-#define LCFIR_R32_PAIR2 1 // 1: the pair table's second half loaded entry by entry as the first half's pairs retire
-#endif
-#ifndef LCFIR_R32_PAD
-#define LCFIR_R32_PAD 1 // T2's rows padded to 17 slots: conflict-free without an XOR swizzle's address math (-5 %)
-#endif
+// Instrumentation hook: the kernel calls Probe::stamp(i, rnd) at each phase
+// boundary i of its unit rnd.  The product's probe does nothing;
+// tools/fft32r_trace.hip passes one that records s_memtime.
+struct R32NoProbe {
+    __device__ static void stamp(int, int) {}
+};
 
-// Phase timestamps for tools/fft32r_trace.hip (off in the product build):
-// lane 0 of every wave of workgroups < 64 records s_memtime at each phase
-// boundary of its 3rd unit.
-#ifdef LCFIR_FFT32R_TRACE
-__device__ unsigned long long g_fft32r_trace[64][8][24];
-#define R32_STAMP(i)                                                                        \
-    do {                                                                                    \
-        if (blockIdx.x < 64 && rnd == 2 && (threadIdx.x & 63) == 0)                         \
-            g_fft32r_trace[blockIdx.x][threadIdx.x >> 6][i] = __builtin_amdgcn_s_memtime(); \
-    } while (0)
-#else
-#define R32_STAMP(i) \
-    do {             \
-    } while (0)
-#endif
+// The pair path's output stores: one vector-memory instruction per register
+// pair, issued after the next unit's split LDS-DMA (r32_dma_part).  The next
+// unit's top waits vmcnt(kR32PairStores): the DMA has landed once at most the
+// stores issued after it are still in flight.  That holds only if no other
+// vector-memory instruction (a scratch spill or reload included) is issued
+// between the DMA and the next unit's top; the build checks every
+// fir_fft32r_kernel for zero scratch (Makefile `check-scratch`).
+constexpr int kR32PairStores = 32;
+// s_waitcnt immediate for vmcnt(n), expcnt and lgkmcnt left at their maxima
+constexpr int r32_vmcnt(int n) { return (n & 15) | ((n >> 4) << 14) | 0x0F70; }
+static_assert(kR32PairStores < 64 && r32_vmcnt(kR32PairStores) == 0x8F70 && r32_vmcnt(0) == kVmcnt0,
+              "vmcnt(n) encoding: low 4 bits in [3:0], high 2 bits in [15:14]");
 
 // LDS work array: one region per wave (T1 / T1 backwards address regions by
 // wave; T2 stays inside its wave's region), 32-lane groups and halves inside
-constexpr int kR32Rg = LCFIR_R32_PAD ? 1088 : 1024; // double2 per region
-constexpr int kR32Gs = LCFIR_R32_PAD ? 544 : 512;
-constexpr int kR32Hs = LCFIR_R32_PAD ? 272 : 256;
+// T2's rows are padded to 17 slots: conflict-free without an XOR swizzle's
+// address math (-5 %)
+constexpr int kR32Row = 17;
+constexpr int kR32Hs = 16 * kR32Row;  // double2 per 32-lane half (16 rows)
+constexpr int kR32Gs = 2 * kR32Hs;    // per 32-lane group
+constexpr int kR32Rg = 2 * kR32Gs;    // per wave region
 constexpr int kR32Work = 8 * kR32Rg;
 // T2 slot of (half base, kappa mod 16, gamma): conflict-free for the writers
 // (8 consecutive gamma) and the readers (16 distinct kappa per read group)
-__device__ __forceinline__ int r32_t2(int base, int kl, int gam) {
-    return LCFIR_R32_PAD ? base + 17 * kl + gam : base + 16 * kl + (gam ^ kl);
-}
+__device__ __forceinline__ int r32_t2(int base, int kl, int gam) { return base + kR32Row * kl + gam; }
 // a T2 reader's slot for register i = gamma; rb = its half base + row offset
-__device__ __forceinline__ int r32_t2r(int rb, int i, int kl) { return LCFIR_R32_PAD ? rb + i : rb + (i ^ kl); }
-constexpr int kR32Row = LCFIR_R32_PAD ? 17 : 16;
+__device__ __forceinline__ int r32_t2r(int rb, int i) { return rb + i; }
 
 // column k1 of lane (wave w, 32-lane group g, half h); mirror columns k1 and
 // 32 - k1 share a group (wave 0 group 0: the self-paired columns 0 and 16)
@@ -246,57 +220,6 @@ __device__ __forceinline__ void dft32(double2 (&a)[32]) {
     dft32_hook(a, [] {});
 }
 
-// a[off + r] *= s0 w^r, r < 16, for a unit w: s_{r+2} = 2 Re(w^2) s_r - s_{r-2}
-// (Chebyshev; two FMAs per power).  Each power is applied as it is made, so
-// only the last four are live.
-__device__ __forceinline__ void r32_chain16(double2 (&a)[32], int off, double2 s0, double2 w) {
-    const double c2 = w.x + w.x;
-    const double q2 = __builtin_fma(c2, c2, -2.0); // 2 Re(w^2)
-    double2 s1 = cmul(s0, w);
-    double2 s2 = make_double2(__builtin_fma(c2, s1.x, -s0.x), __builtin_fma(c2, s1.y, -s0.y));
-    double2 s3 = make_double2(__builtin_fma(c2, s2.x, -s1.x), __builtin_fma(c2, s2.y, -s1.y));
-    a[off] = cmul(a[off], s0);
-    a[off + 1] = cmul(a[off + 1], s1);
-    a[off + 2] = cmul(a[off + 2], s2);
-    a[off + 3] = cmul(a[off + 3], s3);
-#pragma unroll
-    for (int r = 4; r < 16; r += 2) {
-        const double2 n0 = make_double2(__builtin_fma(q2, s2.x, -s0.x), __builtin_fma(q2, s2.y, -s0.y));
-        const double2 n1 = make_double2(__builtin_fma(q2, s3.x, -s1.x), __builtin_fma(q2, s3.y, -s1.y));
-        a[off + r] = cmul(a[off + r], n0);
-        a[off + r + 1] = cmul(a[off + r + 1], n1);
-        s0 = s2;
-        s1 = s3;
-        s2 = n0;
-        s3 = n1;
-    }
-}
-// a[r] *= w^r, r < 32 (r = 0 untouched), the same recurrence
-__device__ __forceinline__ void r32_chain32(double2 (&a)[32], double2 w) {
-    const double c2 = w.x + w.x;
-    const double q2 = __builtin_fma(c2, c2, -2.0);
-    double2 s0 = make_double2(1.0, 0.0), s1 = w;
-    double2 s2 = make_double2(__builtin_fma(c2, w.x, -1.0), c2 * w.y);
-    double2 s3 = make_double2(__builtin_fma(c2, s2.x, -w.x), __builtin_fma(c2, s2.y, -w.y));
-    a[1] = cmul(a[1], s1);
-    a[2] = cmul(a[2], s2);
-    a[3] = cmul(a[3], s3);
-#pragma unroll
-    for (int r = 4; r < 32; r += 2) {
-        const double2 n0 = make_double2(__builtin_fma(q2, s2.x, -s0.x), __builtin_fma(q2, s2.y, -s0.y));
-        const double2 n1 = make_double2(__builtin_fma(q2, s3.x, -s1.x), __builtin_fma(q2, s3.y, -s1.y));
-        a[r] = cmul(a[r], n0);
-        a[r + 1] = cmul(a[r + 1], n1);
-        s0 = s2;
-        s1 = s3;
-        s2 = n0;
-        s3 = n1;
-    }
-}
-
-#ifndef LCFIR_R32_TW
-#define LCFIR_R32_TW 1 // twiddle powers: 1 = anchored chains (~2e-15), 0 = plain Chebyshev recurrence (~6e-14)
-#endif
 // a[off + r] *= s0 w^r, r < R (a multiple of 4), for a unit w, w4 = w^4:
 // anchors A = s0 w^(4m) by complex multiplies, and from each anchor two
 // Chebyshev steps s_(r+1) = 2 Re(w) s_r - s_(r-1) (two FMAs a power).  The
@@ -354,8 +277,9 @@ __device__ __forceinline__ bool r32_interior(const DirectParams &p, int64_t n0) 
 }
 // One LDS-DMA transfer (16 B per lane to LDS byte lds + 16 lane) issued by
 // inline asm: the compiler then does not know it writes LDS, so it adds no
-// vmcnt(0) before the next unit's LDS reads; LCFIR_R32_LATEWAIT's explicit
-// vmcnt(32) orders them instead (every later compiler wait only over-counts).
+// vmcnt(0) before the next unit's LDS reads; the explicit vmcnt(kR32PairStores)
+// at the next unit's top orders them instead (every later compiler wait only
+// over-counts).
 __device__ __forceinline__ void r32_dma_asm(const float *base, uint32_t nbytes, uint32_t lds, int vofs, int sofs) {
     typedef unsigned u4 __attribute__((ext_vector_type(4)));
     const uint64_t a = reinterpret_cast<uint64_t>(base);
@@ -373,22 +297,13 @@ __device__ __forceinline__ void r32_dma_part(const DirectParams &p, int ch, int6
     const int w = j >> 6, lane = j & 63;
     const float *x = p.x + (int64_t)ch * p.x_stride;
     const int64_t w0 = n0 - p.half - p.x_lo;
-    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float *>(x), (short)0, (int)((p.x_hi - p.x_lo) * 4), 0x00020000);
     const int vofs = 4096 * (lane >> 5) + 512 * w + 16 * (lane & 31);
     const int sofs = (int)(w0 * 4);
 #pragma unroll
-    for (int s = s0; s < s1; ++s) {
-#if LCFIR_R32_LATEWAIT
-        (void)rsrc;
+    for (int s = s0; s < s1; ++s)
         r32_dma_asm(x, (uint32_t)((p.x_hi - p.x_lo) * 4),
                     __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(fft_lds_void *)(flds + kR32Rg * w + 64 * s)),
                     vofs, sofs + 8192 * s);
-#else
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (fft_lds_void *)(flds + kR32Rg * w + 64 * s), 16, vofs,
-                                                 sofs + 8192 * s, 0, LCFIR_R32_DMA_AUX);
-#endif
-    }
 }
 __device__ __forceinline__ void r32_stage_samples(const DirectParams &p, int ch, int64_t n0, int j, double2 *flds) {
     const int w = j >> 6, lane = j & 63;
@@ -405,7 +320,7 @@ __device__ __forceinline__ void r32_stage_samples(const DirectParams &p, int ch,
 #pragma unroll
         for (int s = 0; s < 16; ++s)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (fft_lds_void *)(flds + kR32Rg * w + 64 * s), 16, vofs,
-                                                     sofs + 8192 * s, 0, LCFIR_R32_DMA_AUX);
+                                                     sofs + 8192 * s, 0, 0);
     } else {
         float2 v[32];
         fft_load_unit<32>(p, ch, n0, j, v);
@@ -415,34 +330,17 @@ __device__ __forceinline__ void r32_stage_samples(const DirectParams &p, int ch,
     }
 }
 
-// The next unit's samples into L2 while the older waves (threads t < 256)
-// wait at T1's first barrier, so the final phase's LDS-DMA of them (every CU
-// at once) hits L2 instead of queueing on HBM.  One dword per 64-B line,
-// through LDS-DMA into a 256-B area nobody reads (no VGPR destination, no
-// compiler-tracked load: the later vmcnt waits only over-count).  Edge units
-// (window before the channel start) are left to the DMA.
-__device__ __forceinline__ void r32_prefetch_samples(const DirectParams &p, int ch, int64_t n0, int t,
-                                                     fft_lds_void *dummy) {
-    const float *x = p.x + (int64_t)ch * p.x_stride;
-    const int64_t w0 = n0 - p.half - p.x_lo;
-    if (w0 < 0 || w0 >= p.x_hi - p.x_lo) return;
-    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float *>(x), (short)0, (int)((p.x_hi - p.x_lo) * 4), 0x00020000);
-    const int sofs = (int)(w0 * 4);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) // 8 x 256 lines of 64 B = the unit's 128 KiB
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, dummy, 4, 64 * t, sofs + 16384 * i, 0, 0);
-}
-
-// a unit whose outputs take the pair-store path (32 stores per lane)
+// a unit whose outputs take the pair-store path (kR32PairStores per lane)
 __device__ __forceinline__ bool r32_pair_path(const DirectParams &p, int64_t n0, int B) {
     return (p.half & 1) == 0 && n0 >= p.start && (p.end - n0 >= B || ((p.end - n0) & 1) == 0);
 }
 
 // Outputs of one unit: c[2m] = Re out[n], c[2m+1] = -Im out[n], m = j + 512 n,
 // valid for c in [half, L - half); sg = the sign bit waves 4..7 put on odd n
-// (their rotated final DFT32).  Range-checked buffer stores, nt, as
-// fir_fft32.hpp's fft32_store_unit (quad form when half is a multiple of 4).
+// (their rotated final DFT32).  Range-checked buffer stores, nt: 8-byte pairs
+// through a per-unit resource when half is even (r32_pair_path), else one
+// dword per output with explicit range checks (an odd half or a unit that
+// straddles the range's start).
 __device__ __forceinline__ float r32_store_unit(const DirectParams &p, int ch, int64_t n0, int B, int j,
                                                 const double2 (&o)[32], int sg) {
     float *yb = p.y + (int64_t)ch * p.y_stride + (p.start - p.y_lo);
@@ -457,7 +355,6 @@ __device__ __forceinline__ float r32_store_unit(const DirectParams &p, int ch, i
         f0 = __int_as_float(__float_as_int((float)o[n].x) ^ s);
         f1 = __int_as_float(__float_as_int((float)(-o[n].y)) ^ s);
     };
-#if LCFIR_R32_STORE == 2
     if (r32_pair_path(p, n0, B)) {
         // pair stores: lane j's (c, c + 1) = 2 (j + 512 n) + {0, 1} as one 8-byte
         // store through a resource over exactly the unit's valid outputs
@@ -470,8 +367,9 @@ __device__ __forceinline__ float r32_store_unit(const DirectParams &p, int ch, i
             __builtin_amdgcn_make_buffer_rsrc(yb + (n0 - p.start), (short)0, nrec, 0x00020000);
         const int v0 = 8 * j - 4 * cmin;
         using b64_t = decltype(__builtin_amdgcn_raw_buffer_load_b64(yu, 0, 0, 0));
+        static_assert(kR32PairStores == 32, "one pair store per register: the count the next unit's wait assumes");
 #pragma unroll
-        for (int n = 0; n < 32; ++n) {
+        for (int n = 0; n < kR32PairStores; ++n) {
             float f0, f1;
             F(n, f0, f1);
             const int vo = v0 + 4096 * n;
@@ -480,34 +378,6 @@ __device__ __forceinline__ float r32_store_unit(const DirectParams &p, int ch, i
             __builtin_amdgcn_raw_buffer_store_b64(
                 __builtin_bit_cast(b64_t, make_int2(__float_as_int(f0), __float_as_int(f1))), yu, vo, 0,
                 kFft32StoreAux);
-        }
-    } else
-#endif
-    if ((cmin & 3) == 0 && n0 >= p.start && n0 + B <= p.end) {
-        // quad stores: lanes j and j ^ 1 trade one pair (DPP quad_perm [1,0,3,2])
-        const bool odd = j & 1;
-        const int jq = j & ~1;
-        using b128_t = decltype(__builtin_amdgcn_raw_buffer_load_b128(ys, 0, 0, 0));
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            float a0, a1, b0, b1;
-            F(2 * k, a0, a1);
-            F(2 * k + 1, b0, b1);
-            const int ca = 2 * (j + 1024 * k), cb = ca + 1024;
-            const bool oka = ca >= cmin && ca < cmax, okb = cb >= cmin && cb < cmax;
-            pk = fmaxf(pk, fmaxf(oka ? fmaxf(fabsf(a0), fabsf(a1)) : 0.0f, okb ? fmaxf(fabsf(b0), fabsf(b1)) : 0.0f));
-            const int s0 = __float_as_int(odd ? a0 : b0), s1 = __float_as_int(odd ? a1 : b1);
-            const int r0 = __builtin_amdgcn_update_dpp(0, s0, 0xB1, 0xF, 0xF, false);
-            const int r1 = __builtin_amdgcn_update_dpp(0, s1, 0xB1, 0xF, 0xF, false);
-            int4 q;
-            q.x = odd ? r0 : __float_as_int(a0);
-            q.y = odd ? r1 : __float_as_int(a1);
-            q.z = odd ? __float_as_int(b0) : r0;
-            q.w = odd ? __float_as_int(b1) : r1;
-            const int cq = 2 * (jq + 512 * (2 * k + (odd ? 1 : 0)));
-            const bool okq = cq >= cmin && cq < cmax;
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(b128_t, q), ys,
-                                                   okq ? (int)((off + cq) * 4) : (int)0x80000000, 0, kFft32StoreAux);
         }
     } else {
 #pragma unroll
@@ -528,6 +398,18 @@ __device__ __forceinline__ float r32_store_unit(const DirectParams &p, int ch, i
     return pk;
 }
 
+// fft_peak_stage with the wave's slot addressed from its wave-uniform index:
+// the per-lane address fft_peak_stage derives from threadIdx.x was hoisted out
+// of the unit loop and spilled (the kernel's only scratch access, a
+// vector-memory reload on the path between the split DMA and the next unit's
+// vmcnt(kR32PairStores))
+__device__ __forceinline__ void r32_peak_stage(float *pk_lds, float pk) {
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) pk = fmaxf(pk, __shfl_xor(pk, s, 64));
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    if ((threadIdx.x & 63) == 0) pk_lds[wv] = pk;
+}
+
 // The kernel's workgroup barriers order LDS only: __syncthreads()'s release
 // fence would also wait for the wave's global stores (the previous unit's
 // outputs, a fused normalize slice), which no other wave reads.
@@ -546,7 +428,8 @@ __device__ __forceinline__ void r32_bar() {
 // floats, which the older waves (0..3) load, rescale and store while they
 // wait at T1's first barrier and at T1 backwards' first barrier (the younger
 // waves arrive there thousands of cycles later).
-template <int kOut = kFftOutSym, bool kNrm = false> // templates: host-only users emit no kernel stub
+// Probe: phase-boundary hook (R32NoProbe in the product).
+template <int kOut = kFftOutSym, bool kNrm = false, class Probe = R32NoProbe> // templates: host-only users emit no kernel stub
 __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, const double2 *__restrict__ pair,
                                                            const double2 *__restrict__ tw,
                                                            const uint32_t *__restrict__ task, int B, FftGrid gd,
@@ -554,7 +437,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
     extern __shared__ double2 flds[];
     // the pair table's second half entry by entry (-2 %); the fused-rescale
     // kernel keeps the block load (the early loads spill 6 more VGPRs there)
-    constexpr bool kPair2 = LCFIR_R32_PAIR2 && !kNrm;
+    constexpr bool kPair2 = !kNrm;
     bool nrm_on = false;
     double nrm_gain = 1.0;
     if constexpr (kNrm) {
@@ -589,8 +472,6 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
     }
     __builtin_amdgcn_s_waitcnt(kVmcnt0);
     __syncthreads();
-    if (LCFIR_R32_STAGGER > 0 && (blockIdx.x & 1))
-        for (int i = 0; i < LCFIR_R32_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
     uint32_t tk_all = task[threadIdx.x];
     asm volatile("" : "+v"(tk_all));
     float pk_run = 0.0f;
@@ -607,12 +488,10 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
         const int ch = fft_div(u, gd);
         const int64_t n0 = p.seg0 + (int64_t)(u - ch * gd.nseg) * B;
         double2 a[32];
-#if LCFIR_R32_LATEWAIT
-        // the staging transfers have landed; the previous unit's 32 pair
-        // stores (issued after them) may still be in flight
-        __builtin_amdgcn_s_waitcnt(0x8F70);
-#endif
-        R32_STAMP(0);
+        // the staging transfers have landed; the previous unit's pair stores
+        // (issued after them) may still be in flight
+        __builtin_amdgcn_s_waitcnt(r32_vmcnt(kR32PairStores));
+        Probe::stamp(0, rnd);
         // ---- stage 1: the samples out of the wave's region (staged by the
         // previous unit), waves 4..7 negating the odd ones; DFT32; W_16384^(b k1)
         {
@@ -631,33 +510,18 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
         dft32(a);
         {
             // register r holds k1 = r + 16 hi (mod 32): powers w^(16 hi) w^r, w^(16 (1 - hi)) w^(r - 16)
-            const double2 wb = twl[kR32TwB + j], w16 = twl[kR32TwB16 + j], one = make_double2(1.0, 0.0);
-            if (LCFIR_R32_TW) {
-                r32_chain_k1acc(a, wb, w16, hi);
-            } else {
-                r32_chain16(a, 0, csel(hi, w16, one), wb);
-                r32_chain16(a, 16, csel(hi, one, w16), wb);
-            }
+            const double2 wb = twl[kR32TwB + j], w16 = twl[kR32TwB16 + j];
+            r32_chain_k1acc(a, wb, w16, hi);
         }
-        R32_STAMP(1);
+        Probe::stamp(1, rnd);
         // ---- T1 round 1: registers 0..15 into the wave's own region (its lanes
         // read their samples from it above: issue order is enough)
 #pragma unroll
         for (int i = 0; i < 16; ++i) flds[kR32Rg * w + 64 * i + lane] = a[i];
-        R32_STAMP(2);
+        Probe::stamp(2, rnd);
         nrm_half(u, 0, j, wu);
-#if LCFIR_R32_PF
-        if (wu < 4) {
-            const int un1 = fft_unit32(rnd + 1, blockIdx.x, gridDim.x, gd.units);
-            if (un1 < gd.units) {
-                const int cn = fft_div(un1, gd);
-                r32_prefetch_samples(p, cn, p.seg0 + (int64_t)(un1 - cn * gd.nseg) * B, j,
-                                     (fft_lds_void *)(spl + 32));
-            }
-        }
-#endif
         r32_bar();
-        R32_STAMP(3);
+        Probe::stamp(3, rnd);
         if (pk_pending >= 0) {
             if (threadIdx.x == 0) fft_peak_commit(p, pk_pending, pk_lds);
             pk_pending = -1;
@@ -671,9 +535,9 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
 #pragma unroll
             for (int i = 0; i < 16; ++i) c[i] = flds[base + kR32Rg * (i >> 2) + 16 * (i & 3)];
         }
-        R32_STAMP(4);
+        Probe::stamp(4, rnd);
         r32_bar();
-        R32_STAMP(5);
+        Probe::stamp(5, rnd);
         // ---- T1 round 2: registers 16..31 (k1 = 16 + i, or i for waves 4..7)
         // into the region of their column's wave
         {
@@ -684,39 +548,21 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
                 flds[kR32Rg * (home >> 2) + 256 * (home & 3) + base] = a[16 + i];
             }
         }
-        R32_STAMP(6);
+        Probe::stamp(6, rnd);
         r32_bar();
         {
             const int base = kR32Rg * w + 256 * (2 * g + h) + gam;
 #pragma unroll
             for (int i = 0; i < 16; ++i) c[16 + i] = flds[base + 16 * i];
         }
-        R32_STAMP(7);
+        Probe::stamp(7, rnd);
         // ---- stage 2: DFT32 over beta (rotated by 16 h), * (s W_512^gam)^kappa, s = (-1)^h
         double2 pq[16], p2v[8];
-#if LCFIR_R32_PAIRLOAD
-        // the pair table's first half, issued between the DFT32's halves so a
-        // wave whose loads queue behind the CU's other transfers still computes
-        dft32_hook(c, [&] {
-            const double2 *pt = pair + j;
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int i = 0; i < 8; ++i) pq[i] = pt[512 * i];
-#pragma unroll
-            for (int m = 0; m < 4; ++m) p2v[m] = pt[512 * (16 + m)];
-            __builtin_amdgcn_sched_barrier(0);
-        });
-#else
         dft32(c);
-#endif
         double2 wg = twl[kR32TwG + gam];
         if (h) wg = make_double2(-wg.x, -wg.y);
-        if (LCFIR_R32_TW)
-            r32_chain32acc(c, wg);
-        else
-            r32_chain32(c, wg);
-        R32_STAMP(8);
-#if !LCFIR_R32_PAIRLOAD
+        r32_chain32acc(c, wg);
+        Probe::stamp(8, rnd);
         // ---- the pair table's first half, in flight across T2
         {
             const double2 *pt = pair + j;
@@ -725,9 +571,8 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
 #pragma unroll
             for (int m = 0; m < 4; ++m) p2v[m] = pt[512 * (16 + m)];
         }
-#endif
         __builtin_amdgcn_sched_barrier(0);
-        R32_STAMP(9);
+        Probe::stamp(9, rnd);
         // ---- T2: two wave-local rounds (kappa < 16, kappa >= 16) in the wave's region
         uint32_t tk = tk_all;
         asm volatile("" : "+v"(tk)); // per unit: T2's addresses are not hoisted out of the loop
@@ -740,18 +585,18 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
         for (int kl = 0; kl < 16; ++kl) flds[r32_t2(wb2, kl, gam)] = c[kl];
         wave_lds_sync();
 #pragma unroll
-        for (int i = 0; i < 16; ++i) R1[i] = flds[r32_t2r(rb1, i, x1)];
+        for (int i = 0; i < 16; ++i) R1[i] = flds[r32_t2r(rb1, i)];
         wave_lds_sync();
 #pragma unroll
         for (int kl = 0; kl < 16; ++kl) flds[r32_t2(wb2, kl, gam)] = c[16 + kl];
         wave_lds_sync();
 #pragma unroll
-        for (int i = 0; i < 16; ++i) R2[i] = flds[r32_t2r(rb2, i, x2)];
-        R32_STAMP(10);
+        for (int i = 0; i < 16; ++i) R2[i] = flds[r32_t2r(rb2, i)];
+        Probe::stamp(10, rnd);
         // ---- stage 3: DFT16 over gamma -> lambda
         dft16f(R1);
         dft16f(R2);
-        R32_STAMP(11);
+        Probe::stamp(11, rnd);
         // ---- pair step: slot i pairs R1[i] (bin k) with R2[15 - i] (bin N - k);
         // the special lane permutes its registers into that layout first
         const bool sp = wu == 0 && lane == kR32SpecialLane;
@@ -800,7 +645,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
                          R2[15 - i]);
             __builtin_amdgcn_sched_barrier(0);
         }
-        R32_STAMP(12);
+        Probe::stamp(12, rnd);
         if (wu == 0) {
             if (sp) {
                 // back: R1 = [x 15, x 8..14, conj(c8 v8), y 1..7], R2 = [x 0..7, y 8..15]
@@ -822,7 +667,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
         // ---- inverse stage 3: DFT16 over lambda -> gamma (on conj(V))
         dft16f(R1);
         dft16f(R2);
-        R32_STAMP(13);
+        Probe::stamp(13, rnd);
         // ---- T2 backwards (addresses recomputed from laundered words: the 32
         // of T2 would otherwise stay live across the pair step)
         {
@@ -835,36 +680,33 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
             const int sb2 = kR32Rg * wb_ + kR32Gs * gb_ + kR32Hs * ((tkb >> 5) & 1) + kR32Row * y2;
             const int sbw = kR32Rg * wb_ + kR32Gs * gb_ + kR32Hs * hb_;
 #pragma unroll
-            for (int i = 0; i < 16; ++i) flds[r32_t2r(sb1, i, y1)] = R1[i];
+            for (int i = 0; i < 16; ++i) flds[r32_t2r(sb1, i)] = R1[i];
             wave_lds_sync();
 #pragma unroll
             for (int kl = 0; kl < 16; ++kl) c[kl] = flds[r32_t2(sbw, kl, gmb)];
             wave_lds_sync();
 #pragma unroll
-            for (int i = 0; i < 16; ++i) flds[r32_t2r(sb2, i, y2)] = R2[i];
+            for (int i = 0; i < 16; ++i) flds[r32_t2r(sb2, i)] = R2[i];
             wave_lds_sync();
 #pragma unroll
             for (int kl = 0; kl < 16; ++kl) c[16 + kl] = flds[r32_t2(sbw, kl, gmb)];
         }
-        R32_STAMP(14);
+        Probe::stamp(14, rnd);
         // ---- inverse stage 2: * (s W_512^gam)^kappa, DFT32 (outputs rotated by 16 h).
         // The powers are rebuilt, not kept from stage 2 (124 VGPRs across the
         // pair step): the laundered base stops the compiler from reusing them.
         asm volatile("" : "+v"(wg.x), "+v"(wg.y));
-        if (LCFIR_R32_TW)
-            r32_chain32acc(c, wg);
-        else
-            r32_chain32(c, wg);
+        r32_chain32acc(c, wg);
         dft32(c);
         wave_lds_sync();
-        R32_STAMP(15);
+        Probe::stamp(15, rnd);
         // ---- T1 backwards, round 1: registers 0..15 into the wave's own region
 #pragma unroll
         for (int i = 0; i < 16; ++i) flds[kR32Rg * w + 64 * i + lane] = c[i];
-        R32_STAMP(16);
+        Probe::stamp(16, rnd);
         nrm_half(u, 1, j, wu);
         r32_bar();
-        R32_STAMP(17);
+        Probe::stamp(17, rnd);
         {
             // thread b: register r holds k1 = r + 16 hi, from lane (k1, gamma_b)'s register beta_b & 15
             const int base = 64 * ((j >> 4) & 15) + (j & 15);
@@ -874,20 +716,20 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
                 a[r] = flds[kR32Rg * (home >> 2) + 16 * (home & 3) + base];
             }
         }
-        R32_STAMP(18);
+        Probe::stamp(18, rnd);
         r32_bar();
-        R32_STAMP(19);
+        Probe::stamp(19, rnd);
         {
             // registers 16..31: beta = i + 16 (1 - h) -> thread 16 beta + gam's region
             const int base = 4 * kR32Rg * (1 - h) + 64 * (k1 & 15) + gam;
 #pragma unroll
             for (int i = 0; i < 16; ++i) flds[base + kR32Rg * (i >> 2) + 16 * (i & 3)] = c[16 + i];
         }
-        R32_STAMP(20);
+        Probe::stamp(20, rnd);
         r32_bar();
 #pragma unroll
         for (int i = 0; i < 16; ++i) a[16 + i] = flds[kR32Rg * w + 64 * i + lane];
-        R32_STAMP(21);
+        Probe::stamp(21, rnd);
         // vmcnt(0) lgkmcnt(0): the wave's reads of its region have retired (and
         // the compiler's vmcnt accounting ignores LDS-DMA; see fir_fft32.hpp)
         {
@@ -896,16 +738,9 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
             const int un = un1 < gd.units ? un1 : u;
             const int cn = fft_div(un, gd);
             const int64_t nn = p.seg0 + (int64_t)(un - cn * gd.nseg) * B;
-#if LCFIR_R32_DMASPLIT
             const bool split = r32_interior(p, nn);
             if (!split) r32_stage_samples(p, cn, nn, j, flds);
-#else
-            constexpr bool split = false;
-#ifndef LCFIR_R32_NODMA // timing-only diagnostic (wrong outputs): the next unit reuses stale LDS
-            r32_stage_samples(p, cn, nn, j, flds);
-#endif
-#endif
-            R32_STAMP(22);
+            Probe::stamp(22, rnd);
             // ---- final: * W_16384^(b k1), DFT32 over k1 -> n (an interior next
             // unit's DMA issued in quarters between the VALU blocks, so a wave
             // whose transfer waits for the CU's memory queue still computes)
@@ -919,35 +754,24 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
             };
             const double2 wb = twl[kR32TwB + j], w16 = twl[kR32TwB16 + j], one = make_double2(1.0, 0.0);
             part(std::integral_constant<int, 0>{});
-            if (LCFIR_R32_TW) {
+            {
                 const double2 w2 = cmul(wb, wb);
                 const double2 w4 = cmul(w2, w2);
                 r32_chain_anchored<16>(a, 0, csel(hi, w16, one), wb, w4);
                 part(std::integral_constant<int, 1>{});
                 r32_chain_anchored<16>(a, 16, csel(hi, one, w16), wb, w4);
-            } else {
-                r32_chain16(a, 0, csel(hi, w16, one), wb);
-                part(std::integral_constant<int, 1>{});
-                r32_chain16(a, 16, csel(hi, one, w16), wb);
             }
             part(std::integral_constant<int, 2>{});
             dft32_hook(a, [&] { part(std::integral_constant<int, 3>{}); });
         }
-#if LCFIR_R32_LATEWAIT
-        // pair-path units: the DMA wait moves to the next unit's top
+        // pair-path units: the DMA wait moves to the next unit's top (its
+        // vmcnt(kR32PairStores) lets exactly these stores stay in flight);
+        // the other units wait for the staging transfers here
         if (!r32_pair_path(p, n0, B)) __builtin_amdgcn_s_waitcnt(kVmcnt0);
-#else
-        __builtin_amdgcn_s_waitcnt(kVmcnt0); // the staging transfers have landed (stage 1 reads them)
-#endif
-#ifdef LCFIR_R32_NOSTORE // timing-only diagnostic (wrong outputs): no output stores
-        float pk = 0.0f;
-        if (p.start < 0) pk = r32_store_unit(p, ch, n0, B, j, a, hi ? (int)0x80000000 : 0);
-#else
         const float pk = r32_store_unit(p, ch, n0, B, j, a, hi ? (int)0x80000000 : 0);
-#endif
         if (ch != pk_ch) {
             if (p.peak && pk_ch >= 0) {
-                fft_peak_stage(pk_lds, pk_run);
+                r32_peak_stage(pk_lds, pk_run);
                 pk_pending = pk_ch;
                 asm volatile("" : "+v"(pk_pending));
             }
@@ -955,7 +779,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
             pk_ch = ch;
         }
         pk_run = fmaxf(pk_run, pk);
-        R32_STAMP(23);
+        Probe::stamp(23, rnd);
     }
     __builtin_amdgcn_s_waitcnt(kVmcnt0);
     if (p.peak && pk_ch >= 0) {

@@ -298,22 +298,25 @@ std::atomic<int> g_range_profile{0};
 std::mutex g_stats_mu;
 lcfir_range_stats g_stats{};
 
-// [p, p + bytes) lies in page-locked host memory the DMA engine can read
+// [p, p + bytes) lies in ONE page-locked host allocation (hipHostMalloc or
+// hipHostRegister), which the DMA engine can read as a whole.  Checking only
+// the two ends would accept a range that starts in one registration, ends in
+// another and is pageable in between (hipMemcpyAsync resolves the allocation
+// from the start pointer); such a range is treated as pageable.
 bool host_pinned(const void *p, size_t bytes) {
     hipPointerAttribute_t a{};
     if (hipPointerGetAttributes(&a, p) != hipSuccess || a.type != hipMemoryTypeHost) {
         (void)hipGetLastError();
         return false;
     }
-    if (bytes > 1) {
-        hipPointerAttribute_t b{};
-        if (hipPointerGetAttributes(&b, static_cast<const char *>(p) + bytes - 1) != hipSuccess ||
-            b.type != hipMemoryTypeHost) {
-            (void)hipGetLastError();
-            return false;
-        }
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (hipMemGetAddressRange(&base, &size, const_cast<void *>(p)) != hipSuccess || !base) {
+        (void)hipGetLastError();
+        return false;
     }
-    return true;
+    const auto b = reinterpret_cast<uintptr_t>(base), q = reinterpret_cast<uintptr_t>(p);
+    return q >= b && bytes <= size && q - b <= size - bytes;
 }
 
 int ensure_bounce(Staging *st) {
@@ -599,6 +602,21 @@ int lcfir_ctx_fft_info(lcfir_ctx *ctx, int32_t *seg_len, int32_t *parts, int32_t
     *seg_len = ctx->fft.L;
     *parts = ctx->fft.parts;
     *zero_phase = ctx->fft.sym ? 1 : 0;
+    return LCFIR_OK;
+}
+
+int lcfir_ctx_fft_units(lcfir_ctx *ctx, int32_t *outputs, int32_t *kernel, int32_t *nrm_floats) {
+    if (!ctx || !outputs || !kernel || !nrm_floats) return fail(LCFIR_EINVAL, "null argument");
+    *outputs = *kernel = *nrm_floats = 0;
+    if (!lcfir::fft_supported(ctx->ntaps)) return LCFIR_OK;
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return fail(LCFIR_EDEVICE, "hipSetDevice(%d) failed", ctx->device);
+    const int rc = ensure_fft(ctx);
+    if (rc != LCFIR_OK) return rc;
+    *outputs = ctx->fft.B;
+    *kernel = ctx->fft.reg32 ? LCFIR_FFT_KERNEL_L32_REG
+            : ctx->fft.L == lcfir::kFft32L ? LCFIR_FFT_KERNEL_L32_PARK : LCFIR_FFT_KERNEL_L16;
+    *nrm_floats = (int32_t)lcfir::fft_nrm_unit_floats(ctx->fft);
     return LCFIR_OK;
 }
 

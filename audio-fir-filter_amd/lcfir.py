@@ -41,6 +41,8 @@ class LcfirError(RuntimeError):
 PROGRESS_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64)
 
 STAGING_BOUNCE, STAGING_PAGEABLE = 0, 1
+# lcfir_ctx_fft_units' kernel codes (LCFIR_FFT_KERNEL_*)
+FFT_KERNELS = {0: None, 1: "l16", 2: "l32_park", 3: "l32_reg"}
 
 
 class RangeStats(ctypes.Structure):
@@ -68,6 +70,8 @@ _SIGNATURES = {
     "lcfir_ctx_half": ([_ctxp, ctypes.POINTER(_c_i32)], _c_int),
     "lcfir_ctx_fft_info": ([_ctxp, ctypes.POINTER(_c_i32), ctypes.POINTER(_c_i32), ctypes.POINTER(_c_i32)],
                            _c_int),
+    "lcfir_ctx_fft_units": ([_ctxp, ctypes.POINTER(_c_i32), ctypes.POINTER(_c_i32), ctypes.POINTER(_c_i32)],
+                            _c_int),
     "lcfir_ctx_nrm_stats": ([_ctxp, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i64)], _c_int),
     "lcfir_ctx_set_fft_tuning": ([_ctxp, _c_i32, _c_i32, _c_i64, _c_i64], _c_int),
     "lcfir_ctx_ntaps": ([_ctxp, ctypes.POINTER(_c_i32)], _c_int),
@@ -222,6 +226,16 @@ class Filter:
         L, P, Z = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
         _check(load().lcfir_ctx_fft_info(self._ctx, ctypes.byref(L), ctypes.byref(P), ctypes.byref(Z)))
         return {"seg_len": L.value, "parts": P.value, "zero_phase": bool(Z.value)}
+
+    @property
+    def fft_units(self) -> dict:
+        """The plan's unit geometry (lcfir_ctx_fft_units): outputs per segment
+        B, the kernel that runs a unit ("l16", "l32_park", "l32_reg"), and the
+        most floats of a previous file's normalize one unit carries inside the
+        filter launch (0: never fused)."""
+        b, k, f = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        _check(load().lcfir_ctx_fft_units(self._ctx, ctypes.byref(b), ctypes.byref(k), ctypes.byref(f)))
+        return {"outputs": b.value, "kernel": FFT_KERNELS.get(k.value), "nrm_floats": f.value}
 
     @property
     def nrm_stats(self) -> dict:

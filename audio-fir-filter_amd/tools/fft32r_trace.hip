@@ -3,8 +3,7 @@
 // L = 32 768 kernel.  Runs a config-3 shaped launch (8 x 5.76 M samples,
 // 8001 symmetric taps) and prints, per wave, the average shader cycles of each
 // phase of a steady-state unit over 64 workgroups.
-//   hipcc -O3 -std=c++2b --offload-arch=gfx950 -I../csrc -DLCFIR_FFT32R=1 -DLCFIR_FFT32R_TRACE \
-//         fft32r_trace.hip -o fft32r_trace
+//   hipcc -O3 -std=c++2b --offload-arch=gfx950 -I../csrc fft32r_trace.hip -o fft32r_trace
 //   ./fft32r_trace [ntaps] [seg_len] [sym|asym] [nrm]
 // "nrm": every launch also carries a previous file's normalize (FftNrm) of
 // n x nch floats, as config 5's fused form does.
@@ -18,6 +17,16 @@
 #include <vector>
 
 #include "fir_fft.hpp"
+
+// lane 0 of every wave of workgroups < 64 records s_memtime at each phase
+// boundary of its 3rd unit (the kernel's Probe hook)
+__device__ unsigned long long g_fft32r_trace[64][8][24];
+struct TraceProbe {
+    __device__ static void stamp(int i, int rnd) {
+        if (blockIdx.x < 64 && rnd == 2 && (threadIdx.x & 63) == 0)
+            g_fft32r_trace[blockIdx.x][threadIdx.x >> 6][i] = __builtin_amdgcn_s_memtime();
+    }
+};
 
 #define CK(x)                                                                   \
     do {                                                                        \
@@ -123,7 +132,18 @@ int main(int argc, char **argv) {
         }
         std::printf("fused normalize of %lld floats per launch\n", (long long)nrm.count);
     }
-    auto launch = [&]() { return lcfir::fft_launch(plan, p, nch, nullptr, err, with_nrm ? &nrm : nullptr); };
+    if (!plan.reg32) {
+        std::fprintf(stderr, "this plan does not run fir_fft32r_kernel\n");
+        return 1;
+    }
+    // one launch chunk covers the whole channel: fft_launch_group's q for it
+    lcfir::DirectParams q = p;
+    q.seg0 = 0;
+    q.ntaps = plan.ntaps;
+    auto launch = [&]() {
+        return with_nrm ? lcfir::fft32r_launch_one<lcfir::kFftOutSym, true, TraceProbe>(plan, q, nch, nullptr, err, nrm)
+                        : lcfir::fft32r_launch_one<lcfir::kFftOutSym, false, TraceProbe>(plan, q, nch, nullptr, err);
+    };
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
@@ -146,9 +166,8 @@ int main(int argc, char **argv) {
     const int64_t units = (int64_t)((n + plan.B - 1) / plan.B) * nch;
     std::printf("kernel %.4f ms (min %.4f)  (%.1f Gsamples/s), units %lld, units/WG %.2f\n", ms / reps, ms_min / reps,
                 (double)n * nch / (ms / reps * 1e-3) / 1e9, (long long)units, (double)units / plan.cus);
-#ifdef LCFIR_FFT32R_TRACE
     static unsigned long long tr[64][8][24];
-    CK(hipMemcpyFromSymbol(tr, HIP_SYMBOL(lcfir::g_fft32r_trace), sizeof(tr)));
+    CK(hipMemcpyFromSymbol(tr, HIP_SYMBOL(g_fft32r_trace), sizeof(tr)));
     std::printf("%-32s", "phase \\ wave");
     for (int w = 0; w < 8; ++w) std::printf("%8d", w);
     std::printf("%8s\n", "avg");
@@ -169,6 +188,5 @@ int main(int argc, char **argv) {
     std::printf("%-32s", "unit total");
     for (int w = 0; w < 8; ++w) std::printf("%8.0f", total[w]);
     std::printf("\n");
-#endif
     return 0;
 }

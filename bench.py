@@ -362,6 +362,50 @@ class TimedBackend:
         return self._timed(self.inner.filter_normalize_prev, *a, **k)
 
 
+class TimedCollective:
+    """The runner's peak all-reduce with HIP events on the stream it is issued
+    from (the lane's current stream): the span from the step's filter work
+    being done to the reduced peaks being visible there, i.e. the collective
+    plus any wait for the slowest rank."""
+
+    def __init__(self, inner, torch):
+        self.inner, self.torch = inner, torch
+        self.events = []
+        self.record = False
+
+    def __call__(self, peaks):
+        if not self.record:
+            return self.inner(peaks)
+        s = self.torch.cuda.current_stream()
+        e0 = self.torch.cuda.Event(enable_timing=True)
+        e1 = self.torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        self.inner(peaks)
+        e1.record(s)
+        self.events.append((e0, e1))
+
+    def mean_ms(self):
+        if not self.events:
+            return None
+        return sum(a.elapsed_time(b) for a, b in self.events) / len(self.events)
+
+
+def rank_spread(records):
+    """Per-rank figures of an N-rank line (records: one dict per rank, in rank
+    order, from all_gather_object): each numeric field as a list plus its min
+    and max, so an under-scaling SCALE point shows which rank (and which GPU,
+    by PCI bus id) was slow and what the collective cost."""
+    out = {"rank": [r["rank"] for r in records],
+           "device": [r.get("device") for r in records]}
+    for k in ("ms_per_step", "kernel_ms", "allreduce_ms_per_step", "samples"):
+        vals = [r.get(k) for r in records]
+        out[k] = vals
+        num = [v for v in vals if v is not None]
+        out[k + "_min"] = min(num) if num else None
+        out[k + "_max"] = max(num) if num else None
+    return out
+
+
 def preroll(step, seconds, sync, agree=None, batch=8):
     """Untimed steps, in batches, until `seconds` have passed.  Every rank
     must run the same number of steps (a step with a peak exchange is a
@@ -446,8 +490,9 @@ def main():
 
     backend = TimedBackend(batch.DeviceBackend(flt, dev, lanes=args.lanes, own_streams=args.graph == "on"),
                            torch)
+    collective = TimedCollective(batch.torch_allreduce_max(), torch)
     runner = batch.BatchRunner(backend, rank, world, [n] * nfiles, nch, half, args.normalize,
-                               args.peak_scope, batch.torch_allreduce_max(), lanes=args.lanes,
+                               args.peak_scope, collective, lanes=args.lanes,
                                fuse_normalize=not args.no_fuse_normalize, force_exchange=args.force_exchange)
     # synthetic samples; configs 4/5 reuse two generated files to bound host time
     cache = {}
@@ -511,6 +556,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     backend.record = True
+    collective.record = True
     t0 = time.perf_counter()
     for _ in range(n_replay):
         graphed.replay()
@@ -521,6 +567,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     backend.record = False
+    collective.record = False
     backend.set_lane(0)
     launches = len(backend.events)
     overlapped_ms = sum(a.elapsed_time(b) for a, b in backend.events) / max(1, launches)
@@ -536,6 +583,16 @@ def main():
     if not args.no_ingest and runner.shards:
         ingest = ingest_probe(torch, lcfir, file_samples(runner.shards[0].file), bits, dev)
 
+    props = torch.cuda.get_device_properties(dev)
+    mine = {"rank": rank, "device": f"{props.pci_domain_id:04x}:{props.pci_bus_id:02x}:{props.pci_device_id:02x}"
+                                    f" (cuda:{local})",
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "kernel_ms": round(kern_ms, 6),
+            "allreduce_ms_per_step": (round(collective.mean_ms(), 4) if collective.events else None),
+            "samples": my_samples}
+    records = [mine]
+    if world > 1:
+        records = [None] * world
+        dist.all_gather_object(records, mine)
     total_samples = torch.tensor([float(my_samples)], dtype=torch.float64, device=dev)
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
@@ -671,6 +728,9 @@ def main():
             "parity": {"rms_vs_longdouble": rms, "max_ulp": worst_ulp, "positions": npos,
                        "tol": 1e-9, "of": "outputs of the last timed step (rank 0, first shard)"},
             "preroll": {"seconds": round(preroll_s, 3), "steps": preroll_steps},
+            # per-rank spread (value and ms_per_step above are max-based); the
+            # all-reduce time is the peak exchange's HIP-event span per step
+            "ranks": rank_spread(records),
         }
         if ingest is not None:
             line["ingest"] = ingest  # rank 0's

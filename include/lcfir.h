@@ -82,6 +82,18 @@ int lcfir_ctx_ntaps(const lcfir_ctx *ctx, int32_t *ntaps);
  * the filter runs in zero-phase form (linear-phase taps).  All 0 when the tap
  * count is outside the FFT method's range. */
 int lcfir_ctx_fft_info(lcfir_ctx *ctx, int32_t *seg_len, int32_t *parts, int32_t *zero_phase);
+/* Diagnostic: the unit geometry of the same plan.  *outputs: outputs per
+ * overlap-save segment (B = seg_len - taps per partition + 1); *kernel: which
+ * kernel runs a unit (LCFIR_FFT_KERNEL_*); *nrm_floats: the most floats of a
+ * previous file's normalize (lcfir_filter_window_norm_dev) one unit carries
+ * inside the filter launch, 0 when that kernel never carries one.  A call with
+ * U = ceil(outputs of its first launch chunk / B) x nch units fuses the
+ * normalize iff ncount <= U x *nrm_floats (and d_ny is 16-byte aligned).  All
+ * 0 when the tap count is outside the FFT method's range. */
+#define LCFIR_FFT_KERNEL_L16 1      /* fir_fft_f64_kernel: L = 16 384, LDS columns */
+#define LCFIR_FFT_KERNEL_L32_PARK 2 /* fir_fft32_f64_kernel: L = 32 768, two halves + park slab */
+#define LCFIR_FFT_KERNEL_L32_REG 3  /* fir_fft32r_kernel: L = 32 768 held in registers (zero-phase) */
+int lcfir_ctx_fft_units(lcfir_ctx *ctx, int32_t *outputs, int32_t *kernel, int32_t *nrm_floats);
 /* Diagnostic: how many previous-file normalizes (lcfir_filter_window_norm_dev
  * with ncount > 0) this ctx carried inside its filter launch (*fused) and how
  * many it ran as their own pass (*separate) since it was created. */

@@ -1,0 +1,101 @@
+#!/bin/bash
+# One parameterised GPU-box runner (replaces the per-experiment gpu_r0*.sh
+# scripts of rounds 3-4).  Each STEP runs under its own time limit, writes
+# gpurun_out/<TAG>/<n>_<step>.log and prints its tail; the first failure ends
+# the run (no retries).
+#
+# usage (repo root, on the GPU box): bash scripts/gpu_run.sh TAG STEP [STEP ...]
+#   smoke                   __graft_entry__.smoke()
+#   suite[:ARGS]            pytest -m gpu (ARGS: extra pytest args, e.g. a file)
+#   bench[:ARGS]            bench.py --steps 20 --warmup 5 ARGS (the driver's shape)
+#   ab:V1,V2:REPS[:ARGS]    alternating bench lines of abvar/V1.so, abvar/V2.so, ...
+#                           (scripts/build_variant.sh builds them; "prod" = this tree's library)
+#   parity:V[:ARGS]         the FFT parity + fuzz tests with abvar/V.so in place
+#   fuzz:SEED0,CASES,NORM   seeded fuzz campaign (tests/test_gpu_fuzz.py)
+#   trace[:ARGS]            tools/fft32r_trace phase timeline (default 4001 32768)
+#   prof[:ARGS]             rocprofv3 --kernel-trace --stats of a bench line + the
+#                           exclusive launches from its trace
+#   pmc[:ARGS]              FETCH_SIZE / WRITE_SIZE / VALU-instruction passes (one
+#                           rocprofv3 --pmc run each) + pmc_summary.json
+#   dropin[:ARGS]           tests/cpp/dropin_bench
+#   gpus2[:ARGS]            bench.py --gpus 2 rehearsal on one device (gloo)
+# Words in ARGS are separated by spaces (quote the whole STEP).
+set -u -o pipefail
+ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+cd "$ROOT"
+TAG=${1:?tag}; shift
+OUT="$ROOT/gpurun_out/$TAG"
+mkdir -p "$OUT"
+N=0
+run() { # name timeout cmd...
+    local name=$1 t=$2; shift 2
+    N=$((N + 1))
+    local log="$OUT/${N}_$name.log"
+    echo "== $N $name ($(date +%T)): $*" | cut -c1-300
+    timeout -k 10 "$t" "$@" > "$log" 2>&1
+    local rc=$?
+    tail -4 "$log" | cut -c1-3000
+    if [ $rc -ne 0 ]; then echo "!! $name failed rc=$rc"; tail -40 "$log"; exit $rc; fi
+}
+brief() { # the bench line's headline fields
+    python3 -c 'import json,sys
+for l in sys.stdin:
+    if l.startswith("{"):
+        d=json.loads(l); r=d["roofline"]; p=d.get("parity",{})
+        print(d["value"], d["ms_per_step"], r["kernel_ms"], r["frac"], p.get("rms_vs_longdouble"), p.get("max_ulp"))'
+}
+LIB=audio-fir-filter_amd/liblcfir.so
+cp "$LIB" /tmp/liblcfir_prod.so
+restore() { cp /tmp/liblcfir_prod.so "$LIB"; }
+trap restore EXIT
+for S in "$@"; do
+    kind=${S%%:*}
+    rest=""; [ "$kind" != "$S" ] && rest=${S#*:}
+    case $kind in
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    suite) run suite 1500 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread $rest ;;
+    bench) run bench 400 python bench.py --steps 20 --warmup 5 $rest ;;
+    ab)
+        vs=${rest%%:*}; r2=${rest#*:}; reps=${r2%%:*}; args=""; [ "$r2" != "$reps" ] && args=${r2#*:}
+        for rep in $(seq 1 "$reps"); do
+            for v in ${vs//,/ }; do
+                if [ "$v" = prod ]; then restore; else cp "abvar/$v.so" "$LIB"; fi
+                N=$((N + 1)); log="$OUT/${N}_ab_${v}_$rep.log"
+                timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-ingest $args > "$log" 2>&1 \
+                    || { echo "!! ab $v failed"; tail -20 "$log"; exit 1; }
+                echo "$v rep$rep $(brief < "$log")" | tee -a "$OUT/ab.txt"
+            done
+        done
+        restore ;;
+    parity)
+        v=${rest%%:*}; args=""; [ "$v" != "$rest" ] && args=${rest#*:}
+        cp "abvar/$v.so" "$LIB"
+        run "parity_$v" 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu \
+            tests/test_gpu_parity.py tests/test_gpu_fuzz.py tests/test_gpu_baseline_configs.py $args
+        restore ;;
+    fuzz)
+        IFS=, read -r s0 nc nn <<< "$rest"
+        LCFIR_FUZZ_SEED0=$s0 LCFIR_FUZZ_CASES=$nc LCFIR_FUZZ_NORM_CASES=$nn \
+            run fuzz 900 python -u -m pytest tests/test_gpu_fuzz.py -m gpu -q -p no:cacheprovider \
+            --timeout 120 --timeout-method thread ;;
+    trace) run trace 120 audio-fir-filter_amd/tools/fft32r_trace ${rest:-4001 32768} ;;
+    prof)
+        (cd /tmp && export TMPDIR=/tmp && run prof 600 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof" -o bench -- \
+            python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-parity --no-ingest $rest) || exit 1
+        python3 scripts/trace_exclusive.py "$OUT/prof/bench_kernel_trace.csv" > "$OUT/exclusive_from_trace.json"
+        cat "$OUT/exclusive_from_trace.json" | head -c 600; echo ;;
+    pmc)
+        i=0
+        for c in FETCH_SIZE WRITE_SIZE "SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64"; do
+            i=$((i + 1))
+            (cd /tmp && export TMPDIR=/tmp && run "pmc_$i" 300 rocprofv3 --pmc $c --kernel-include-regex 'fir_' -f csv \
+                -d "$OUT/pmc/p_$i" -o pmc -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline \
+                --no-parity --no-ingest $rest) || exit 1
+        done
+        python3 scripts/pmc_summary.py "$OUT/pmc" --json "$OUT/pmc_summary.json" > /dev/null && echo "pmc summary ok" ;;
+    dropin) run dropin 600 tests/cpp/dropin_bench ${rest:---threads 1,16,ref --reps 3} ;;
+    gpus2) LCFIR_BENCH_SHARE_DEVICE=1 run gpus2 400 python bench.py --gpus 2 --steps 10 --warmup 2 $rest ;;
+    *) echo "unknown step $S"; exit 2 ;;
+    esac
+done
+echo "== done"

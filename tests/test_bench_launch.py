@@ -95,3 +95,55 @@ def test_usable_cpus_cgroup_v1(tmp_path):
     (tmp_path / "cpu" / "cpu.cfs_quota_us").write_text("-1\n")
     assert bench.cgroup_cpu_quota(str(tmp_path)) is None
     assert bench.cgroup_cpu_quota(str(tmp_path / "missing")) is None
+
+
+def test_rank_spread_reduction():
+    """The N > 1 line's per-rank block: lists in rank order, min and max of
+    each figure (value and ms_per_step stay max-based)."""
+    recs = [{"rank": 0, "device": "0000:05:00 (cuda:0)", "ms_per_step": 1.30, "kernel_ms": 1.10,
+             "allreduce_ms_per_step": 0.05, "samples": 10},
+            {"rank": 1, "device": "0000:15:00 (cuda:1)", "ms_per_step": 1.45, "kernel_ms": 1.12,
+             "allreduce_ms_per_step": 0.21, "samples": 10}]
+    r = bench.rank_spread(recs)
+    assert r["rank"] == [0, 1] and r["device"] == ["0000:05:00 (cuda:0)", "0000:15:00 (cuda:1)"]
+    assert r["ms_per_step"] == [1.30, 1.45] and r["ms_per_step_min"] == 1.30 and r["ms_per_step_max"] == 1.45
+    assert r["kernel_ms_max"] == 1.12 and r["allreduce_ms_per_step_min"] == 0.05
+    # no exchange on the step: the all-reduce fields are null, not 0
+    recs = [dict(d, allreduce_ms_per_step=None) for d in recs]
+    r = bench.rank_spread(recs)
+    assert r["allreduce_ms_per_step"] == [None, None] and r["allreduce_ms_per_step_max"] is None
+
+
+def _gather_worker(rank, world, port, q):
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    mine = {"rank": rank, "device": f"cpu{rank}", "ms_per_step": 1.0 + rank, "kernel_ms": 0.5,
+            "allreduce_ms_per_step": 0.1 * (rank + 1), "samples": 100 * (rank + 1)}
+    records = [None] * world
+    dist.all_gather_object(records, mine)
+    if rank == 0:
+        q.put(bench.rank_spread(records))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_rank_spread_gathered_over_gloo():
+    """bench.py's all_gather_object of the per-rank records, world 2 on gloo."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gather_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    r = q.get(timeout=100)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert r["rank"] == [0, 1] and r["device"] == ["cpu0", "cpu1"]
+    assert r["ms_per_step_max"] == 2.0 and r["samples"] == [100, 200]
+    assert r["allreduce_ms_per_step_max"] == pytest.approx(0.2)

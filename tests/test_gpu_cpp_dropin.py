@@ -168,6 +168,33 @@ def test_apply_range_staging_modes(oracle_mod, mode, ntaps):
         finally:
             lib.lcfir_host_free(px)
             lib.lcfir_host_free(py)
+        if mode == "bounce":
+            # a caller range that starts in one pinned registration and ends in
+            # another, pageable in between: not one page-locked allocation, so
+            # it is staged (both ends pinned is not enough)
+            import torch
+            rt = torch.cuda.cudart()
+            page = 1 << 16
+            raw = np.zeros(n + 3 * page, np.float32)
+            a0 = (-raw.ctypes.data) % page // 4
+            hx = raw[a0:a0 + n]
+            hx[:] = x
+            lo_len = (page * 4) & ~(page - 1)
+            hi_off = (4 * n - lo_len) & ~(page - 1)
+            hi_len = (4 * n - hi_off + page - 1) & ~(page - 1)  # into raw's padding: whole pages
+            regs = [(hx.ctypes.data, lo_len), (hx.ctypes.data + hi_off, hi_len)]
+            done = []
+            try:
+                for ptr, ln in regs:
+                    assert int(rt.cudaHostRegister(ptr, ln, 0)) == 0
+                    done.append(ptr)
+                y = np.full(n, 7.0, np.float32)
+                flt.apply_range(hx, y, 0, n)
+                assert np.array_equal(y, want)
+                assert lcfir.range_stats(reset=True)["staged_calls"] == 1
+            finally:
+                for ptr in done:
+                    rt.cudaHostUnregister(ptr)
     finally:
         lcfir.staging_set_mode("pageable")  # the library's default
     idx = np.r_[np.arange(0, 20), np.arange(n - 20, n), np.arange(1000, n, 100_003)]

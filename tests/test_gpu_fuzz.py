@@ -18,7 +18,11 @@ both methods.  Every case against the oracle at sampled positions:
 A second set fuzzes lcfir_filter_window_norm_dev (a previous file's normalize
 carried by the filter call) against the separate filter + normalize calls.
 About a third of the FFT cases of both sets force the L = 32 768 segment
-(_seg32), whose normalize is never fused (a separate pass).
+(_seg32): linear-phase filters then run the register kernel (fir_fft32r.hpp,
+whose launch carries the normalize in two halves of up to kNrmK32 blocks per
+unit), the others the park-slab kernel (never fused).  The fused / separate
+switch is sized from the plan itself (lcfir_ctx_fft_units), and every case
+checks which of the two the library took (lcfir_ctx_nrm_stats).
 
 LCFIR_FUZZ_CASES / LCFIR_FUZZ_NORM_CASES / LCFIR_FUZZ_SEED0 widen or shift the
 seed range for a longer campaign (scripts/gpu_fuzz.sh); the defaults are the
@@ -35,7 +39,6 @@ RMS_TOL = 1e-9
 SEED0 = int(os.environ.get("LCFIR_FUZZ_SEED0", "0"))
 N_CASES = int(os.environ.get("LCFIR_FUZZ_CASES", "120"))
 N_NORM_CASES = int(os.environ.get("LCFIR_FUZZ_NORM_CASES", "40"))
-NRM_SLICE_MAX = 14 * 1024  # floats of the previous buffer one FFT unit rescales (fir_fft.hpp kNrmK)
 
 
 def _max_ulps(a, b, floor=1e-12):
@@ -151,21 +154,22 @@ def _norm_case(seed):
     method = "direct" if ntaps <= 1601 and rng.random() < 0.3 else "fft"
     nch = int(rng.integers(1, 4))
     n = int(rng.choice([1, 7, ntaps // 2 + 1, 20_000, 123_457, 300_001]))
-    # units of a one-partition FFT launch (B = L - T + 1): counts around
-    # units x the per-unit slice straddle the fused / separate-pass switch.
-    # Designed (linear-phase) filters from 4 001 taps run the register kernel
-    # (L = 32 768, two halves of 14 Ki floats per unit); the others L = 16 384
-    # (19 201 taps as 2 x 9 601)
     designed = rng.random() < 0.6
-    if designed and ntaps >= 4001:
-        B, per_unit = 32768 - ntaps + 1, 2 * NRM_SLICE_MAX
-    else:
-        B, per_unit = 16384 - (ntaps if ntaps <= 10925 else 9601) + 1, NRM_SLICE_MAX
-    boundary = -(-n // B) * nch * per_unit
+    return rng, ntaps, method, nch, n, designed
+
+
+def _norm_params(rng, n, nch, units):
+    """count, offset, peaks, force of a case.  units: the filter's
+    fft_units.  A one-partition FFT launch of U = ceil(n / B) x nch units
+    carries the normalize iff count <= U x nrm_floats (a 16-B aligned buffer):
+    the counts straddle that switch (the limit itself, +-1 float, +-1 block)."""
+    B, cap = max(1, units["outputs"]), units["nrm_floats"]
+    blk = 2048 if units["kernel"] == "l32_reg" else 1024
+    boundary = -(-n // B) * nch * cap if cap else -(-n // B) * nch * 1024
     count = int(rng.choice([
         1, 3, int(rng.integers(1, 5_000)), int(rng.integers(1, boundary + 1)),
-        int(rng.integers(1, boundary + 1)), boundary, boundary + int(rng.integers(-8, 9)),
-        int(rng.integers(boundary, 2 * boundary + 1))]))
+        int(rng.integers(1, boundary + 1)), boundary, boundary + 1, max(1, boundary - blk), boundary + blk,
+        boundary + int(rng.integers(-8, 9)), int(rng.integers(boundary, 2 * boundary + 1))]))
     if rng.random() < 0.05:
         count = 0  # a plain filter call
     offset = int(rng.choice([0, 0, 0, 0, 0, 1, 2, 3, 4]))  # floats: 16-B aligned when offset % 4 == 0
@@ -174,7 +178,8 @@ def _norm_case(seed):
     if rng.random() < 0.5:
         peaks[int(rng.integers(npeak))] = np.float32(rng.uniform(0.01, 4.0))
     force = bool(rng.random() < 0.4)
-    return rng, ntaps, method, nch, n, count, offset, peaks, force, designed
+    fused = bool(cap and count and count <= boundary and offset % 4 == 0)
+    return max(0, count), offset, peaks, force, fused
 
 
 @pytest.mark.parametrize("seed", range(SEED0, SEED0 + N_NORM_CASES))
@@ -186,16 +191,23 @@ def test_random_norm_case(oracle_mod, seed):
     ProcessFile.cp:98-101 decision."""
     import torch  # before lcfir: one HIP runtime in the process
     import lcfir as lc
-    rng, ntaps, method, nch, n, count, offset, peaks, force, designed = _norm_case(seed)
+    rng, ntaps, method, nch, n, designed = _norm_case(seed)
     if designed:
         taps = oracle_mod.design_lowcut(float(rng.uniform(5.0, 300.0)), 48000.0, ntaps)
     else:
         taps = rng.standard_normal(ntaps) / np.sqrt(ntaps)
-    x = np.ascontiguousarray(np.rint(rng.uniform(-0.9, 0.9, (nch, n)) * 2 ** 23) / 2 ** 23, np.float32)
-    prev = (rng.standard_normal(count + offset) * 0.5).astype(np.float32)
     flt = lc.Filter(taps, method=method)
     if method == "fft" and _seg32(seed):
         flt.set_fft_tuning(seg_len=32768)
+    units = flt.fft_units
+    if method == "fft" and designed and ntaps >= 4001:
+        # linear-phase filters from ~4 000 taps run the register kernel
+        assert units["kernel"] == "l32_reg", (seed, units)
+    count, offset, peaks, force, want_fused = _norm_params(rng, n, nch, units)
+    if method != "fft":
+        want_fused = False
+    x = np.ascontiguousarray(np.rint(rng.uniform(-0.9, 0.9, (nch, n)) * 2 ** 23) / 2 ** 23, np.float32)
+    prev = (rng.standard_normal(count + offset) * 0.5).astype(np.float32)
     dx = torch.from_numpy(x).cuda()
     res = []
     for fused in (False, True):
@@ -214,7 +226,9 @@ def test_random_norm_case(oracle_mod, seed):
         torch.cuda.synchronize()
         res.append((dy.cpu().numpy(), dpk.cpu().numpy(), dprev.cpu().numpy()))
     (y0, p0, r0), (y1, p1, r1) = res
-    case = (seed, ntaps, method, nch, n, count, offset, peaks.tolist(), force)
+    case = (seed, ntaps, method, nch, n, count, offset, peaks.tolist(), force, units)
+    st = flt.nrm_stats
+    assert (st["fused"], st["separate"]) == ((1, 0) if want_fused else (0, 1 if count else 0)), (case, st)
     assert np.array_equal(y0, y1) and np.array_equal(p0, p1), case
     assert np.array_equal(r0, r1), case
     pk = np.float32(peaks.max())

@@ -637,11 +637,12 @@ def test_fft_auto_seg_len(lc, oracle_mod, ntaps, n, nch, want_L):
 
 
 def test_fft_auto_seg_len_follows_the_channel(lc, oracle_mod):
-    """The automatic choice depends on the channel's length, not on the first
-    call's range: a ctx whose first call is a 50 000-output range of a
-    3 M-sample channel (the reference's per-thread chunk, a rank's share of a
-    split file) picks the same segment length as one whose first call is the
-    whole channel, so the range's bytes equal the whole-channel call's."""
+    """The automatic choice is a function of the taps alone, not of the
+    channel or of the first call's range: a ctx whose first call is a
+    50 000-output range of a 3 M-sample channel (the reference's per-thread
+    chunk, a rank's share of a split file) picks the same segment length as one
+    whose first call is the whole channel, so the range's bytes equal the
+    whole-channel call's."""
     import synth
     taps = oracle_mod.design_lowcut(20.0, 48000.0, 12001)
     n = 3_000_000
@@ -687,7 +688,8 @@ def test_fft_plan_independent_of_first_call(lc, oracle_mod, ntaps):
 @pytest.mark.parametrize("method,ntaps,seg_len,zero_phase", [
     ("direct", 15, 0, True), ("direct", 97, 0, True), ("direct", 801, 0, True), ("direct", 4003, 0, True),
     ("fft", 4001, 16384, True), ("fft", 4003, 16384, True), ("fft", 4003, 16384, False),
-    ("fft", 4005, 32768, True), ("fft", 4003, 32768, False), ("fft", 19203, 16384, True)])
+    ("fft", 4005, 32768, True), ("fft", 4003, 32768, True), ("fft", 4003, 32768, False),
+    ("fft", 19203, 16384, True)])
 def test_edge_outputs_every_window_alignment(lc, oracle_mod, method, ntaps, seg_len, zero_phase):
     """Outputs next to a window edge: the whole channel's first and last T + 256
     outputs, and windowed calls whose window [x_lo, x_hi) starts d = 0..3
