@@ -4,9 +4,11 @@
 // 8001 symmetric taps) and prints, per wave, the average shader cycles of each
 // phase of a steady-state unit over 64 workgroups.
 //   hipcc -O3 -std=c++2b --offload-arch=gfx950 -I../csrc fft32r_trace.hip -o fft32r_trace
-//   ./fft32r_trace [ntaps] [seg_len] [sym|asym] [nrm]
+//   ./fft32r_trace [ntaps] [seg_len] [sym|asym] [nrm|-] [cus]
 // "nrm": every launch also carries a previous file's normalize (FftNrm) of
-// n x nch floats, as config 5's fused form does.
+// n x nch floats, as config 5's fused form does.  cus: persistent-grid size
+// (default: every CU); fewer workgroups than CUs leaves the chip's memory
+// system to fewer units in flight (is a phase's cost per CU or chip-wide?).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -86,7 +88,9 @@ int main(int argc, char **argv) {
         std::fprintf(stderr, "plan: %s\n", err.c_str());
         return 1;
     }
-    std::printf("plan: L %d, parts %d, zero-phase %d, B %d\n", plan.L, plan.parts, (int)plan.sym, plan.B);
+    if (argc > 5) plan.cus = std::atoi(argv[5]);
+    std::printf("plan: L %d, parts %d, zero-phase %d, B %d, grid %d\n", plan.L, plan.parts, (int)plan.sym, plan.B,
+                plan.cus);
     lcfir::DirectParams p{};
     p.x = dx;
     p.x_lo = 0;

@@ -6,17 +6,22 @@
 # product tree never carries experiment switches;
 # scripts/gpu_run.sh's ab: and parity: steps time and check the variants.
 # usage: bash scripts/build_variant.sh NAME [PATCH]    (no PATCH: the product as NAME)
+# Also builds tools/fft32r_trace from the patched source as abvar/NAME.trace.
 set -euo pipefail
 ROOT="$(cd "$(dirname "$0")/.." && pwd)"
-NAME=${1:?name}; PATCH=${2:-}
+NAME=${1:?name}; PATCH=${2:+$(realpath "$2")}
 W=$(mktemp -d /tmp/variant_XXXX)
 trap 'rm -rf "$W"' EXIT
 cp -r "$ROOT/audio-fir-filter_amd" "$ROOT/include" "$W/"
 rm -f "$W/audio-fir-filter_amd/liblcfir.so"
-if [ -n "$PATCH" ]; then (cd "$W" && patch -p1 --quiet < "$(realpath "$PATCH")"); fi
+if [ -n "$PATCH" ]; then (cd "$W" && patch -p1 --quiet < "$PATCH"); fi
 make -C "$W/audio-fir-filter_amd" liblcfir.so > "$W/build.log" 2>&1 || { tail -30 "$W/build.log"; exit 1; }
 mkdir -p "$ROOT/abvar"
 cp "$W/audio-fir-filter_amd/liblcfir.so" "$ROOT/abvar/$NAME.so"
 cp "$W/audio-fir-filter_amd/liblcfir.remarks" "$ROOT/abvar/$NAME.remarks"
+# the phase-trace tool of the same source (abvar/NAME.trace: gpu_run.sh trace:ARGS takes TRACE=...)
+/opt/rocm/bin/hipcc -O3 -std=c++2b --offload-arch=gfx950 -I"$W/audio-fir-filter_amd/csrc" \
+    "$W/audio-fir-filter_amd/tools/fft32r_trace.hip" -o "$ROOT/abvar/$NAME.trace" > "$W/trace.log" 2>&1 \
+    || { tail -20 "$W/trace.log"; exit 1; }
 grep -A9 "fir_fft32r_kernelILi4ELb0" "$W/audio-fir-filter_amd/liblcfir.remarks" | grep -E "VGPRs|Spill|Scratch" | sed 's/.*remark: *//; s/ \[-Rpass.*//' | tr '\n' ' '
 echo " -> abvar/$NAME.so"

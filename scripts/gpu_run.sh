@@ -13,11 +13,16 @@
 #   parity:V[:ARGS]         the FFT parity + fuzz tests with abvar/V.so in place
 #   fuzz:SEED0,CASES,NORM   seeded fuzz campaign (tests/test_gpu_fuzz.py)
 #   trace[:ARGS]            tools/fft32r_trace phase timeline (default 4001 32768)
+#   vtrace:V[:ARGS]         the same tool built from variant V's source (abvar/V.trace)
 #   prof[:ARGS]             rocprofv3 --kernel-trace --stats of a bench line + the
 #                           exclusive launches from its trace
 #   pmc[:ARGS]              FETCH_SIZE / WRITE_SIZE / VALU-instruction passes (one
 #                           rocprofv3 --pmc run each) + pmc_summary.json
+#   pmcre:REGEX[:ARGS]      FETCH_SIZE / WRITE_SIZE passes over the kernels matching REGEX
+#   tool:NAME[:ARGS]        audio-fir-filter_amd/tools/NAME (a built development tool)
 #   dropin[:ARGS]           tests/cpp/dropin_bench
+#   dropin_nosdma[:ARGS]    the same with HSA_ENABLE_SDMA=0 (copies by blit kernels)
+#   vdropin:V[:ARGS]        the same over variant V's library
 #   gpus2[:ARGS]            bench.py --gpus 2 rehearsal on one device (gloo)
 # Words in ARGS are separated by spaces (quote the whole STEP).
 set -u -o pipefail
@@ -79,21 +84,38 @@ for S in "$@"; do
             run fuzz 900 python -u -m pytest tests/test_gpu_fuzz.py -m gpu -q -p no:cacheprovider \
             --timeout 120 --timeout-method thread ;;
     trace) run trace 120 audio-fir-filter_amd/tools/fft32r_trace ${rest:-4001 32768} ;;
+    vtrace) # vtrace:V[:ARGS] -- the phase trace of variant V (abvar/V.trace)
+        v=${rest%%:*}; args=""; [ "$v" != "$rest" ] && args=${rest#*:}
+        run "trace_$v" 120 "abvar/$v.trace" ${args:-4001 32768} ;;
     prof)
         (cd /tmp && export TMPDIR=/tmp && run prof 600 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof" -o bench -- \
             python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-parity --no-ingest $rest) || exit 1
         python3 scripts/trace_exclusive.py "$OUT/prof/bench_kernel_trace.csv" > "$OUT/exclusive_from_trace.json"
         cat "$OUT/exclusive_from_trace.json" | head -c 600; echo ;;
-    pmc)
-        i=0
-        for c in FETCH_SIZE WRITE_SIZE "SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64"; do
+    pmc|pmcre)
+        # pmcre:REGEX[:ARGS] -- the kernels matching REGEX (default 'fir_'), traffic passes only
+        re='fir_'; passes=(FETCH_SIZE WRITE_SIZE "SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64")
+        if [ "$kind" = pmcre ]; then
+            re=${rest%%:*}; r2=""; [ "$re" != "$rest" ] && r2=${rest#*:}; rest=$r2; passes=(FETCH_SIZE WRITE_SIZE)
+        fi
+        d="$OUT/$kind$N"; i=0
+        for c in "${passes[@]}"; do
             i=$((i + 1))
-            (cd /tmp && export TMPDIR=/tmp && run "pmc_$i" 300 rocprofv3 --pmc $c --kernel-include-regex 'fir_' -f csv \
-                -d "$OUT/pmc/p_$i" -o pmc -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline \
+            (cd /tmp && export TMPDIR=/tmp && run "${kind}_$i" 300 rocprofv3 --pmc $c --kernel-include-regex "$re" -f csv \
+                -d "$d/p_$i" -o pmc -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline \
                 --no-parity --no-ingest $rest) || exit 1
         done
-        python3 scripts/pmc_summary.py "$OUT/pmc" --json "$OUT/pmc_summary.json" > /dev/null && echo "pmc summary ok" ;;
+        python3 scripts/pmc_summary.py "$d" --json "$d/pmc_summary.json" > /dev/null && echo "pmc summary ok: $d" ;;
+    tool) # tool:NAME[:ARGS] -- a development tool under audio-fir-filter_amd/tools
+        t=${rest%%:*}; args=""; [ "$t" != "$rest" ] && args=${rest#*:}
+        run "tool_$t" 300 "audio-fir-filter_amd/tools/$t" $args ;;
     dropin) run dropin 600 tests/cpp/dropin_bench ${rest:---threads 1,16,ref --reps 3} ;;
+    dropin_nosdma) HSA_ENABLE_SDMA=0 run dropin_nosdma 600 tests/cpp/dropin_bench ${rest:---threads 1,16,ref --reps 3} ;;
+    vdropin) # vdropin:V[:ARGS] -- tests/cpp/dropin_bench over variant V's library
+        v=${rest%%:*}; args=""; [ "$v" != "$rest" ] && args=${rest#*:}
+        cp "abvar/$v.so" "$LIB"
+        run "dropin_$v" 600 tests/cpp/dropin_bench ${args:---threads 1,16,ref --reps 3}
+        restore ;;
     gpus2) LCFIR_BENCH_SHARE_DEVICE=1 run gpus2 400 python bench.py --gpus 2 --steps 10 --warmup 2 $rest ;;
     *) echo "unknown step $S"; exit 2 ;;
     esac
