@@ -485,6 +485,31 @@ int launch_normalize(float *d_y, int64_t stride, int32_t nch, int64_t n, const u
     return LCFIR_OK;
 }
 
+// Change the ctx's FFT tuning: launches already queued may still read the
+// old plan's tables, so wait for them, then free the plan (or retire it, if a
+// captured graph holds it); the next launch builds one with the new tuning.
+template <class F>
+int retune(lcfir_ctx *ctx, F &&set) {
+    DeviceGuard g(ctx->device);
+    if (!g.ok) return fail(LCFIR_EDEVICE, "hipSetDevice(%d) failed", ctx->device);
+    std::lock_guard<std::mutex> lk(ctx->fft_mu);
+    {
+        std::lock_guard<std::mutex> lk2(ctx->streams_mu);
+        for (hipStream_t s : ctx->used) (void)hipStreamSynchronize(s);
+    }
+    if (ctx->plan_captured) {
+        // a captured graph still passes these tables to its kernels
+        ctx->retired_plans.push_back(ctx->fft);
+        ctx->fft = lcfir::FftPlan{};
+        ctx->plan_captured = false;
+    } else {
+        lcfir::fft_plan_free(ctx->fft, ctx->own);
+    }
+    LCFIR_HIP(hipStreamSynchronize(ctx->own));
+    set(ctx->tune);
+    return LCFIR_OK;
+}
+
 } // namespace
 
 extern "C" {
@@ -615,6 +640,7 @@ int lcfir_ctx_fft_units(lcfir_ctx *ctx, int32_t *outputs, int32_t *kernel, int32
     if (rc != LCFIR_OK) return rc;
     *outputs = ctx->fft.B;
     *kernel = ctx->fft.reg32 ? LCFIR_FFT_KERNEL_L32_REG
+            : ctx->fft.reg16 ? LCFIR_FFT_KERNEL_L16_REG
             : ctx->fft.L == lcfir::kFft32L ? LCFIR_FFT_KERNEL_L32_PARK : LCFIR_FFT_KERNEL_L16;
     *nrm_floats = (int32_t)lcfir::fft_nrm_unit_floats(ctx->fft);
     return LCFIR_OK;
@@ -636,29 +662,21 @@ int lcfir_ctx_set_fft_tuning(lcfir_ctx *ctx, int32_t seg_len, int32_t zero_phase
     if (zero_phase != 0 && zero_phase != 1) return fail(LCFIR_EINVAL, "zero_phase must be 0 or 1");
     if (chunk != 0 && chunk < 4096) return fail(LCFIR_EINVAL, "chunk must be 0 or >= 4096 outputs");
     if (max_units < 0 || max_units >= ((int64_t)1 << 31)) return fail(LCFIR_EINVAL, "max_units out of range");
-    DeviceGuard g(ctx->device);
-    if (!g.ok) return fail(LCFIR_EDEVICE, "hipSetDevice(%d) failed", ctx->device);
-    std::lock_guard<std::mutex> lk(ctx->fft_mu);
-    // launches already queued may still read the old plan's tables: wait for
-    // them, then free the plan; the next launch builds one with the new tuning
-    {
-        std::lock_guard<std::mutex> lk2(ctx->streams_mu);
-        for (hipStream_t s : ctx->used) (void)hipStreamSynchronize(s);
-    }
-    if (ctx->plan_captured) {
-        // a captured graph still passes these tables to its kernels
-        ctx->retired_plans.push_back(ctx->fft);
-        ctx->fft = lcfir::FftPlan{};
-        ctx->plan_captured = false;
-    } else {
-        lcfir::fft_plan_free(ctx->fft, ctx->own);
-    }
-    LCFIR_HIP(hipStreamSynchronize(ctx->own));
-    ctx->tune.seg_len = seg_len;
-    ctx->tune.zero_phase = zero_phase;
-    ctx->tune.chunk = chunk;
-    ctx->tune.max_units = max_units;
-    return LCFIR_OK;
+    return retune(ctx, [&](lcfir::FftTuning &t) {
+        t.seg_len = seg_len;
+        t.zero_phase = zero_phase;
+        t.chunk = chunk;
+        t.max_units = max_units;
+    });
+}
+
+int lcfir_ctx_set_fft_family(lcfir_ctx *ctx, int family) {
+    if (!ctx) return fail(LCFIR_EINVAL, "ctx is null");
+    static_assert(LCFIR_FFT_FAMILY_DEFAULT == lcfir::kFamilyDefault && LCFIR_FFT_FAMILY_LDS == lcfir::kFamilyLds &&
+                  LCFIR_FFT_FAMILY_REGISTER == lcfir::kFamilyRegister);
+    if (family != LCFIR_FFT_FAMILY_DEFAULT && family != LCFIR_FFT_FAMILY_REGISTER && family != LCFIR_FFT_FAMILY_LDS)
+        return fail(LCFIR_EINVAL, "unknown FFT kernel family %d", family);
+    return retune(ctx, [&](lcfir::FftTuning &t) { t.family = family; });
 }
 
 // [lo, hi) of lcfir_ctx_window, clipped to [0, n); start < end

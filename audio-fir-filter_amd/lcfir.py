@@ -42,7 +42,8 @@ PROGRESS_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64)
 
 STAGING_BOUNCE, STAGING_PAGEABLE = 0, 1
 # lcfir_ctx_fft_units' kernel codes (LCFIR_FFT_KERNEL_*)
-FFT_KERNELS = {0: None, 1: "l16", 2: "l32_park", 3: "l32_reg"}
+FFT_KERNELS = {0: None, 1: "l16", 2: "l32_park", 3: "l32_reg", 4: "l16_reg"}
+FFT_FAMILIES = {"default": 0, "lds": 1, "register": 2}
 
 
 class RangeStats(ctypes.Structure):
@@ -74,6 +75,7 @@ _SIGNATURES = {
                             _c_int),
     "lcfir_ctx_nrm_stats": ([_ctxp, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i64)], _c_int),
     "lcfir_ctx_set_fft_tuning": ([_ctxp, _c_i32, _c_i32, _c_i64, _c_i64], _c_int),
+    "lcfir_ctx_set_fft_family": ([_ctxp, _c_int], _c_int),
     "lcfir_ctx_ntaps": ([_ctxp, ctypes.POINTER(_c_i32)], _c_int),
     "lcfir_ctx_window": ([_ctxp, _c_i64, _c_i64, _c_i64, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i64)], _c_int),
     "lcfir_apply_range": ([_ctxp, _vp, _c_i64, _vp, _c_i64, _c_i64, PROGRESS_FN, _vp], _c_int),
@@ -250,6 +252,13 @@ class Filter:
         every setting; the defaults are the product's)."""
         _check(load().lcfir_ctx_set_fft_tuning(self._ctx, int(seg_len), 1 if zero_phase else 0, int(chunk),
                                                int(max_units)))
+
+    def set_fft_family(self, family: str = "default"):
+        """lcfir_ctx_set_fft_family for zero-phase single-partition plans:
+        "default" (fir_fft32r at L = 32 768, the LDS-column kernel at 16 384),
+        "register" (fir_fft16r at 16 384 too) or "lds" (the LDS-column
+        kernels everywhere)."""
+        _check(load().lcfir_ctx_set_fft_family(self._ctx, FFT_FAMILIES[family]))
 
     @property
     def ntaps(self) -> int:

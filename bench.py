@@ -61,6 +61,9 @@ def parse():
     ap.add_argument("--ntaps", type=int, default=4001)
     ap.add_argument("--seg-len", type=int, default=0, choices=[0, 16384, 32768],
                     help="FFT segment length (0 = the library's choice)")
+    ap.add_argument("--fft-family", default="default", choices=["default", "lds", "register"],
+                    help="FFT kernel family for zero-phase single-partition plans (lcfir_ctx_set_fft_family): "
+                         "register = fir_fft16r at L = 16 384 too")
     ap.add_argument("--general-form", action="store_true",
                     help="FFT: the general pair table even for linear-phase taps (zero-phase form off)")
     ap.add_argument("--bits", type=int, default=24, help="0 = float32 source")
@@ -426,13 +429,13 @@ def preroll(step, seconds, sync, agree=None, batch=8):
 
 
 
-def fft_kernel_name(info):
-    """The FFT kernel a plan runs (fir_fft.hpp fft_reg32): zero-phase
-    single-partition L = 32 768 plans the register-resident fir_fft32r_kernel,
-    other L = 32 768 plans fir_fft32_f64_kernel, L = 16 384 fir_fft_f64_kernel."""
-    if info["seg_len"] == 32768:
-        return "fir_fft32r_kernel" if info["parts"] == 1 and info["zero_phase"] else "fir_fft32_f64_kernel"
-    return "fir_fft_f64_kernel"
+KERNEL_NAMES = {"l16": "fir_fft_f64_kernel", "l32_park": "fir_fft32_f64_kernel", "l32_reg": "fir_fft32r_kernel",
+                "l16_reg": "fir_fft16r_kernel"}
+
+
+def fft_kernel_name(units):
+    """The FFT kernel a plan runs, from lcfir_ctx_fft_units."""
+    return KERNEL_NAMES[units["kernel"]]
 
 def main():
     args = parse()
@@ -486,6 +489,8 @@ def main():
     flt = lcfir.Filter(taps, device=local, method=args.method)
     if args.seg_len or args.general_form:
         flt.set_fft_tuning(seg_len=args.seg_len, zero_phase=not args.general_form)
+    if args.fft_family != "default":
+        flt.set_fft_family(args.fft_family)
     method = flt.method
 
     backend = TimedBackend(batch.DeviceBackend(flt, dev, lanes=args.lanes, own_streams=args.graph == "on"),
@@ -631,9 +636,11 @@ def main():
             except (OSError, ValueError):
                 continue
             plan = flt.fft_info if method == "fft" else {}
+            kname = fft_kernel_name(flt.fft_units) if method == "fft" else "fir_direct_f64_kernel"
             if tj.get("method") == method and tj.get("ntaps") == args.ntaps and \
                     tj.get("samples_per_launch") == samples_per_launch and \
-                    tj.get("seg_len", 16384 if method == "fft" else None) == plan.get("seg_len"):
+                    tj.get("seg_len", 16384 if method == "fft" else None) == plan.get("seg_len") and \
+                    tj.get("kernel", kname) == kname:
                 traffic = tj.get("hbm_bytes_per_launch")
                 f64_flops = tj.get("f64_flops_per_launch")
                 valu_insts = tj.get("valu_insts_per_launch")
@@ -676,7 +683,7 @@ def main():
                 "workload": wl[args.config] + f", {args.ntaps}-tap low-cut",
                 "files": nfiles, "channels": nch, "samples_per_channel": n,
                 "ntaps": args.ntaps, "method": method,
-                "fft_plan": flt.fft_info if method == "fft" else None,
+                "fft_plan": dict(flt.fft_info, kernel=fft_kernel_name(flt.fft_units)) if method == "fft" else None,
                 "parallelism": f"{world} rank(s), files sharded by batch.plan_shards",
                 "normalize": bool(args.normalize), "peak_scope": args.peak_scope,
                 "peak_exchange": runner.exchange,
@@ -701,7 +708,7 @@ def main():
                 "frac_step_note": "4 B x samples per step per GPU / ms_per_step / 8 TB/s (whole step: "
                                   "launch gaps, collective, normalize passes, lane overlap included)",
                 "traffic": traffic,
-                "kernel": "fir_direct_f64_kernel" if method == "direct" else fft_kernel_name(flt.fft_info),
+                "kernel": "fir_direct_f64_kernel" if method == "direct" else fft_kernel_name(flt.fft_units),
                 "kernel_ms": round(kern_ms, 6),
                 "kernel_ms_note": f"exclusive: {kern_launches} launches of the filter alone on one "
                                   f"stream right after the pre-roll (HIP events on that stream)",

@@ -93,6 +93,7 @@ int lcfir_ctx_fft_info(lcfir_ctx *ctx, int32_t *seg_len, int32_t *parts, int32_t
 #define LCFIR_FFT_KERNEL_L16 1      /* fir_fft_f64_kernel: L = 16 384, LDS columns */
 #define LCFIR_FFT_KERNEL_L32_PARK 2 /* fir_fft32_f64_kernel: L = 32 768, two halves + park slab */
 #define LCFIR_FFT_KERNEL_L32_REG 3  /* fir_fft32r_kernel: L = 32 768 held in registers (zero-phase) */
+#define LCFIR_FFT_KERNEL_L16_REG 4  /* fir_fft16r_kernel: L = 16 384 held in registers, two workgroups per CU (zero-phase) */
 int lcfir_ctx_fft_units(lcfir_ctx *ctx, int32_t *outputs, int32_t *kernel, int32_t *nrm_floats);
 /* Diagnostic: how many previous-file normalizes (lcfir_filter_window_norm_dev
  * with ncount > 0) this ctx carried inside its filter launch (*fused) and how
@@ -114,6 +115,17 @@ int lcfir_ctx_nrm_stats(const lcfir_ctx *ctx, int64_t *fused, int64_t *separate)
  * with launches on the same ctx. */
 int lcfir_ctx_set_fft_tuning(lcfir_ctx *ctx, int32_t seg_len, int32_t zero_phase, int64_t chunk,
                              int64_t max_units);
+/* Which kernel family runs the ctx's zero-phase single-partition plans:
+ * DEFAULT = the transform held in registers at L = 32 768 (fir_fft32r), the
+ * LDS-column kernel at L = 16 384; REGISTER = the register kernels at both
+ * lengths (fir_fft16r at 16 384: two workgroups per CU); LDS = the LDS-column
+ * kernels (fir_fft_f64_kernel, fir_fft32_f64_kernel), which every other plan
+ * runs.  Outputs agree within 1 f32 ulp either way (tests run each); waits for
+ * the ctx's queued launches and drops its plan, as lcfir_ctx_set_fft_tuning. */
+#define LCFIR_FFT_FAMILY_DEFAULT 0
+#define LCFIR_FFT_FAMILY_LDS 1
+#define LCFIR_FFT_FAMILY_REGISTER 2
+int lcfir_ctx_set_fft_family(lcfir_ctx *ctx, int family);
 /* Input window [*lo, *hi) (within [0, n)) of a channel of n samples that
  * makes a call for outputs [start, end) reproduce the whole-channel call's
  * outputs bit for bit, whatever the range: the partition invariance of
