@@ -1640,18 +1640,28 @@ inline int64_t fft_chunk(const FftPlan &plan) {
 // work array + twiddles + 8 f32 peak slots + the special lane's 32 double2
 constexpr size_t kR32LdsBytes = sizeof(double2) * (size_t)(kR32Work + kR32Tw + 2 + 32);
 
-template <int kOut, class Probe = R32NoProbe>
-inline bool fft16r_launch_one(const FftPlan &plan, const DirectParams &q, int nch, hipStream_t s, std::string &err) {
+template <int kOut, bool kNrm = false, class Probe = R32NoProbe>
+inline bool fft16r_launch_one(const FftPlan &plan, const DirectParams &q, int nch, hipStream_t s, std::string &err,
+                              FftNrm nrm = FftNrm{}) {
     static const bool attr = [] {
-        return hipFuncSetAttribute(reinterpret_cast<const void *>(&fir_fft16r_kernel<kOut, Probe>),
+        return hipFuncSetAttribute(reinterpret_cast<const void *>(&fir_fft16r_kernel<kOut, kNrm, Probe>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kR16LdsBytes) == hipSuccess;
     }();
     (void)attr;
     const int64_t nseg = (q.end - q.seg0 + plan.B - 1) / plan.B;
     const int64_t units = nseg * nch; // < 2^31 (fft_launch)
     const int64_t grid = std::min<int64_t>(units, (int64_t)kR16WgPerCu * plan.cus);
-    hipLaunchKernelGGL((fir_fft16r_kernel<kOut, Probe>), dim3((unsigned)grid), dim3(kR16NT), kR16LdsBytes, s, q,
-                       plan.d_pair, plan.d_tw, plan.d_task, plan.B, fft_grid(nseg, units), plan.c8[0].x);
+    if constexpr (kNrm) {
+        // whole 1 024-float blocks per unit, at most kNrmK16 (fft_nrm_fusable)
+        const int64_t per = (nrm.count + units - 1) / units;
+        nrm.slice = (per + 1023) / 1024 * 1024;
+        if (nrm.slice > (int64_t)kNrmK16 * 1024) {
+            err = "normalize slice too large to fuse";
+            return false;
+        }
+    }
+    hipLaunchKernelGGL((fir_fft16r_kernel<kOut, kNrm, Probe>), dim3((unsigned)grid), dim3(kR16NT), kR16LdsBytes, s,
+                       q, plan.d_pair, plan.d_tw, plan.d_task, plan.B, fft_grid(nseg, units), plan.c8[0].x, nrm);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         err = hipGetErrorString(e);
@@ -1726,8 +1736,8 @@ inline bool fft_launch_one(const FftPlan &plan, const DirectParams &q, int part,
     if constexpr (kOut == kFftOutSym)
         if (plan.reg32) return fft32r_launch_one<kOut, kNrm>(plan, q, nch, s, err, nrm);
     if (plan.reg16) {
-        if constexpr (kOut == kFftOutSym && !kNrm) return fft16r_launch_one<kOut>(plan, q, nch, s, err);
-        err = "fir_fft16r_kernel runs zero-phase filters without a fused normalize only";
+        if constexpr (kOut == kFftOutSym) return fft16r_launch_one<kOut, kNrm>(plan, q, nch, s, err, nrm);
+        err = "fir_fft16r_kernel runs zero-phase filters only";
         return false;
     }
     if constexpr (!kNrm)
@@ -1835,7 +1845,8 @@ inline bool fft_launch_group(const FftPlan &plan, const DirectParams &p, int nch
 // lcfir_ctx_fft_units' nrm_floats (tests size the fused / separate switch
 // from it).
 inline int64_t fft_nrm_unit_floats(const FftPlan &plan) {
-    if (plan.parts != 1 || plan.reg16) return 0; // fir_fft16r_kernel carries no normalize
+    if (plan.parts != 1) return 0;
+    if (plan.reg16) return (int64_t)kNrmK16 * 1024;
     if (plan.reg32) return (int64_t)kNrmK32 * 2048;
     return plan.L == kFftL ? (int64_t)kNrmK * 1024 : 0;
 }

@@ -45,6 +45,9 @@ constexpr int kR16Tw = 256 + 16;
 constexpr int kR16SpecialLane = 0;     // of wave 0
 constexpr size_t kR16PairTable = (size_t)24 * kR16NT; // double2: (p1, q2) [16][256], (p2 even, p2 odd) [8][256]
 constexpr int kR16PairStores = 32;     // one 8-byte store per register pair
+// a previous file's normalize carried by the launch (FftNrm): up to kNrmK16
+// blocks of 1 024 floats per unit, one float4 per thread and block
+constexpr int kNrmK16 = 16;
 // LDS: work array, twiddles, 4 peak slots (one double2 of room), the special lane's 32 double2
 constexpr size_t kR16LdsBytes = sizeof(double2) * (size_t)(kR16Work + kR16Tw + 2 + 32);
 static_assert(kR16WgPerCu * kR16LdsBytes <= 160 * 1024, "two workgroups per CU must fit the 160 KiB LDS");
@@ -179,12 +182,24 @@ __device__ __forceinline__ void r16_peak_commit(const DirectParams &p, int ch, c
 // (fft_unit32), zero-phase single-partition filters (kFftOutSym).  pair:
 // kR16PairTable (r16_plan_tables); tw: kR16Tw twiddles; task: 256
 // r16_task_word; c8: the special lane's bin-N/2 coefficient (real).
-template <int kOut = kFftOutSym, class Probe = R32NoProbe> // templates: host-only users emit no kernel stub
+// kNrm: the launch also rescales a previous file's outputs (FftNrm, the
+// normalize_kernel rule): unit u takes floats [u slice, (u + 1) slice), loaded
+// with the unit's samples and stored before its stage 1 -- the other
+// workgroup on the CU computes through the loads' latency.
+template <int kOut = kFftOutSym, bool kNrm = false, class Probe = R32NoProbe> // host-only users emit no stub
 __global__ __launch_bounds__(kR16NT, 2) void fir_fft16r_kernel(DirectParams p, const double2 *__restrict__ pair,
                                                               const double2 *__restrict__ tw,
                                                               const uint32_t *__restrict__ task, int B, FftGrid gd,
-                                                              double c8) {
+                                                              double c8, FftNrm nrm) {
     extern __shared__ double2 flds[];
+    bool nrm_on = false;
+    double nrm_gain = 1.0;
+    if constexpr (kNrm) {
+        float pkv = 0.0f;
+        for (int i = 0; i < nrm.npeak; ++i) pkv = fmaxf(pkv, __uint_as_float(nrm.peak[i]));
+        nrm_on = (pkv > 1.0f || nrm.force) && pkv > 0.0f;
+        nrm_gain = 1.0 / (double)pkv;
+    }
     double2 *twl = flds + kR16Work; // kR16Tw twiddles, then 4 f32 peak slots, then the special lane's scratch
     for (int i = threadIdx.x; i < kR16Tw; i += kR16NT) twl[i] = tw[i];
     float *pk_lds = reinterpret_cast<float *>(twl + kR16Tw);
@@ -210,6 +225,14 @@ __global__ __launch_bounds__(kR16NT, 2) void fir_fft16r_kernel(DirectParams p, c
         {
             float2 v[32];
             r16_load_unit(p, ch, n0, j, v);
+            if constexpr (kNrm) {
+                // the unit's normalize slice: loaded behind the samples, rescaled and
+                // stored before stage 1 (an inactive launch loads through an empty
+                // resource: no traffic, nothing stored)
+                float4 nv[kNrmK16];
+                fft_nrm_load<kNrmK16>(nrm, u, j, nrm_on, nv);
+                if (nrm_on) fft_nrm_store<kNrmK16>(nrm, u, j, nrm_gain, nv);
+            }
 #pragma unroll
             for (int n = 0; n < 32; ++n) a[n] = make_double2((double)v[n].x, (double)v[n].y);
         }

@@ -30,7 +30,7 @@ def r16_filter(lc, taps, **tuning):
     flt.set_fft_family("register")
     u = flt.fft_units
     assert u["kernel"] == "l16_reg" and u["outputs"] == 16384 - len(taps) + 1, u
-    assert u["nrm_floats"] == 0  # the normalize runs as its own pass
+    assert u["nrm_floats"] == 16 * 1024  # kNrmK16 blocks of 1 024 floats per unit
     return flt
 
 
@@ -132,11 +132,17 @@ def test_fft16r_edge_outputs_every_window_alignment(lc, oracle_mod, ntaps):
             assert max_ulps(yw[c], ref) <= 1 and rms(yw[c], ref) <= RMS_TOL, (c, start, x_lo)
 
 
-def test_fft16r_family_switch_and_normalize(lc, oracle_mod):
+@pytest.mark.parametrize("count,offset,peak,force", [(50_000, 0, 2.5, False), (50_000, 1, 2.5, False),
+                                                    (16 * 1024 * 18, 0, 0.5, True), (16 * 1024 * 18 + 1, 0, 3.0, False),
+                                                    (7, 0, 0.75, False)])
+def test_fft16r_family_switch_and_normalize(lc, oracle_mod, count, offset, peak, force):
     """lcfir_ctx_set_fft_family moves a ctx between kernels (the default
     family keeps the LDS-column kernel at 16 384); a previous file's
-    normalize on the register kernel runs as its own pass with the same
-    bytes as the separate calls."""
+    normalize carried by the register kernel's launch (every unit rescales
+    its slice before its stage 1) gives the same bytes as the separate calls:
+    fused up to 16 Ki floats per unit (the 18-unit launch's limit, and one
+    float past it: its own pass), an unaligned buffer its own pass, peaks
+    below 1 without force a no-op."""
     import torch
     taps = oracle_mod.design_lowcut(20.0, 48000.0, 4001)
     flt = lc.Filter(taps, method="fft")
@@ -150,20 +156,28 @@ def test_fft16r_family_switch_and_normalize(lc, oracle_mod):
     rng = np.random.default_rng(3)
     n, nch = 100_000, 2
     x = np.ascontiguousarray(np.rint(rng.uniform(-0.9, 0.9, (nch, n)) * 2 ** 23) / 2 ** 23, np.float32)
-    prev = (rng.standard_normal(50_000) * 0.5).astype(np.float32)
+    prev = (rng.standard_normal(count + offset) * 0.5).astype(np.float32)
+    units = -(-n // flt.fft_units["outputs"]) * nch
+    assert units == 18
     dx = torch.from_numpy(x).cuda()
     res = []
     for fused in (False, True):
         dy = torch.empty((nch, n), dtype=torch.float32, device="cuda")
         dpk = torch.zeros(1, dtype=torch.float32, device="cuda")
         dprev = torch.from_numpy(prev.copy()).cuda()
-        dppk = torch.tensor([2.5], dtype=torch.float32, device="cuda")
+        dppk = torch.tensor([peak], dtype=torch.float32, device="cuda")
+        view = dprev[offset:]
         if fused:
-            flt.filter_window_norm_dev(dx, 0, n, n, n, nch, dy, 0, n, 0, n, dpk, 0, dprev, prev.size, dppk, 1, False)
+            flt.filter_window_norm_dev(dx, 0, n, n, n, nch, dy, 0, n, 0, n, dpk, 0, view, count, dppk, 1, force)
         else:
             flt.filter_window_dev(dx, 0, n, n, n, nch, dy, 0, n, 0, n, dpk, peak_stride=0)
-            lc.normalize_dev(dprev, prev.size, 1, prev.size, dppk, 1, False)
+            lc.normalize_dev(view, count, 1, count, dppk, 1, force)
         torch.cuda.synchronize()
         res.append((dy.cpu().numpy(), dpk.cpu().numpy(), dprev.cpu().numpy()))
     assert all(np.array_equal(a, b) for a, b in zip(res[0], res[1]))
-    assert flt.nrm_stats == {"fused": 0, "separate": 1}
+    want_fused = offset % 4 == 0 and count <= units * 16 * 1024
+    assert flt.nrm_stats == ({"fused": 1, "separate": 0} if want_fused else {"fused": 0, "separate": 1})
+    body = prev[offset:]
+    if peak > 1.0 or force:
+        body = (body.astype(np.float64) * (1.0 / np.float64(np.float32(peak)))).astype(np.float32)
+    assert np.array_equal(res[1][2][offset:], body) and np.array_equal(res[1][2][:offset], prev[:offset])
