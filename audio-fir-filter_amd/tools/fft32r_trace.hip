@@ -25,10 +25,24 @@
 // lane 0 of every wave of workgroups < 64 records s_memtime at each phase
 // boundary of its 3rd unit (the kernel's Probe hook)
 __device__ unsigned long long g_fft32r_trace[64][8][24];
+// residency: per workgroup its CU (HW_ID with the XCC id), the realtime of its
+// first unit's start and of its last unit's end (100 MHz, chip-wide)
+constexpr int kOccMax = 2048;
+__device__ unsigned long long g_occ[kOccMax][3];
+__device__ int g_last_stamp;
 struct TraceProbe {
     __device__ static void stamp(int i, int rnd) {
         if (blockIdx.x < 64 && rnd == 2 && (threadIdx.x & 63) == 0)
             g_fft32r_trace[blockIdx.x][threadIdx.x >> 6][i] = __builtin_amdgcn_s_memtime();
+        if (threadIdx.x == 0 && blockIdx.x < kOccMax) {
+            if (i == 0 && rnd == 0) {
+                const unsigned hw = __builtin_amdgcn_s_getreg(0xF804); // hwreg(HW_REG_HW_ID)
+                const unsigned xcc = __builtin_amdgcn_s_getreg(0xF814); // hwreg(HW_REG_XCC_ID)
+                g_occ[blockIdx.x][0] = ((unsigned long long)xcc << 32) | hw;
+                g_occ[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
+            }
+            if (i == g_last_stamp) g_occ[blockIdx.x][2] = __builtin_amdgcn_s_memrealtime();
+        }
     }
 };
 
@@ -98,6 +112,10 @@ int main(int argc, char **argv) {
     }
     if (argc > 5) plan.cus = std::atoi(argv[5]);
     const bool r16 = plan.reg16;
+    {
+        const int last = r16 ? 18 : 23;
+        CK(hipMemcpyToSymbol(HIP_SYMBOL(g_last_stamp), &last, sizeof(int)));
+    }
     std::printf("plan: L %d, parts %d, zero-phase %d, B %d, grid %d\n", plan.L, plan.parts, (int)plan.sym, plan.B,
                 plan.cus);
     lcfir::DirectParams p{};
@@ -182,6 +200,39 @@ int main(int argc, char **argv) {
     const int64_t units = (int64_t)((n + plan.B - 1) / plan.B) * nch;
     std::printf("kernel %.4f ms (min %.4f)  (%.1f Gsamples/s), units %lld, units/WG %.2f\n", ms / reps, ms_min / reps,
                 (double)n * nch / (ms / reps * 1e-3) / 1e9, (long long)units, (double)units / plan.cus);
+    {
+        // workgroups resident at once per CU (from the last timed launch)
+        static unsigned long long occ[kOccMax][3];
+        CK(hipMemcpyFromSymbol(occ, HIP_SYMBOL(g_occ), sizeof(occ)));
+        const int nwg = (int)std::min<int64_t>((int64_t)units, (int64_t)(r16 ? 2 : 1) * plan.cus);
+        std::vector<std::pair<unsigned long long, int>> ev; // (time, +1/-1) per CU key
+        std::vector<unsigned long long> keys;
+        for (int b = 0; b < std::min(nwg, kOccMax); ++b) {
+            // CU identity: XCC, SE (bits 13..15), SH (12), CU (8..11)
+            const unsigned long long key = (occ[b][0] >> 32) << 16 | ((occ[b][0] >> 8) & 0xFF);
+            keys.push_back(key);
+        }
+        std::vector<unsigned long long> uk = keys;
+        std::sort(uk.begin(), uk.end());
+        uk.erase(std::unique(uk.begin(), uk.end()), uk.end());
+        int maxc = 0;
+        double sum_max = 0;
+        for (unsigned long long k : uk) {
+            std::vector<std::pair<unsigned long long, int>> e;
+            for (int b = 0; b < (int)keys.size(); ++b)
+                if (keys[b] == k) {
+                    e.push_back({occ[b][1], 1});
+                    e.push_back({occ[b][2], -1});
+                }
+            std::sort(e.begin(), e.end());
+            int c = 0, m = 0;
+            for (auto &x : e) m = std::max(m, c += x.second);
+            maxc = std::max(maxc, m);
+            sum_max += m;
+        }
+        std::printf("residency: %d workgroups on %zu CUs; max resident per CU %d, mean of per-CU max %.2f\n",
+                    (int)keys.size(), uk.size(), maxc, uk.empty() ? 0.0 : sum_max / (double)uk.size());
+    }
     static unsigned long long tr[64][8][24];
     CK(hipMemcpyFromSymbol(tr, HIP_SYMBOL(g_fft32r_trace), sizeof(tr)));
     const int nw = r16 ? 4 : 8, nph = r16 ? kPhases16 : kPhases;
