@@ -8,7 +8,9 @@
 //     (FilterCore.h:20-27) on host buffers, re-entrant for the concurrent
 //     disjoint-range calls of ProcessFile.cp:71-78.  Each call borrows a
 //     staging slot (stream + device buffers) from a per-device pool, copies
-//     x[start-half, end+half) in, runs the kernel, copies y[start,end) out;
+//     x[start-half, end+half) in, runs the kernel, copies y[start,end) out
+//     (page-locked caller buffers through the device's two link queues, one
+//     per direction, so concurrent calls move data both ways at once);
 //   * device-pointer entry points that never synchronise the host.
 // No CPU fallback exists: if the device or the kernels are unusable every
 // call fails with LCFIR_EDEVICE and a message.
@@ -291,7 +293,58 @@ struct Staging {
     void *h_bounce[2] = {nullptr, nullptr}; // pinned, kBounceBytes each (lazily)
     hipEvent_t bev[2] = {nullptr, nullptr}; // the last DMA touching h_bounce[b] is done
     hipEvent_t tev[4] = {};                 // lcfir_range_profile: H2D start/end, kernel end, D2H end
+    // link path (pinned caller buffers): slot stream ready / H2D landed /
+    // kernel done, and the blocking-sync end of the call
+    hipEvent_t ev_pre = nullptr, ev_in = nullptr, ev_k = nullptr, done = nullptr;
+    bool linked = false; // this call queued copies on the device's link queues
 };
+
+// The host link's two directions, shared by every call on a device
+// (page-locked caller buffers only).  ROCm 7.2 on MI355X moves 57 GB/s one
+// way and 97 GB/s both ways at once when ONE stream carries each direction,
+// but 52-63 GB/s in total when eight streams split the same bytes
+// (tools/pcie_duplex.hip, profiles/r05_dropin/); the 16 concurrent calls of
+// ProcessFile.cp:71-78 each on its own stream ran their copies one after the
+// other (a rocprofv3 memory-copy trace of tests/cpp/dropin_bench).  So every
+// call's H2D goes on the device's `in` queue and its D2H on the `out` queue, in
+// call order, while its kernel runs on the call's own slot stream between
+// them (stream events order the three).
+struct Link {
+    std::mutex in_mu, out_mu; // enqueue order = issue order on each queue
+    hipStream_t in = nullptr, out = nullptr;
+};
+std::mutex g_link_mu;
+std::vector<Link *> g_links; // per device, created on first use, never destroyed
+
+Link *device_link(int device) {
+    std::lock_guard<std::mutex> lk(g_link_mu);
+    if ((int)g_links.size() <= device) g_links.resize((size_t)device + 1, nullptr);
+    Link *&l = g_links[(size_t)device];
+    if (!l) {
+        auto *n = new Link;
+        if (hipStreamCreateWithFlags(&n->in, hipStreamNonBlocking) != hipSuccess ||
+            hipStreamCreateWithFlags(&n->out, hipStreamNonBlocking) != hipSuccess) {
+            if (n->in) (void)hipStreamDestroy(n->in);
+            delete n;
+            return nullptr;
+        }
+        l = n;
+    }
+    return l;
+}
+
+int ensure_link_events(Staging *st) {
+    for (hipEvent_t *e : {&st->ev_pre, &st->ev_in, &st->ev_k})
+        if (!*e && hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) {
+            *e = nullptr;
+            return fail(LCFIR_EDEVICE, "event creation failed");
+        }
+    if (!st->done && hipEventCreateWithFlags(&st->done, hipEventBlockingSync | hipEventDisableTiming) != hipSuccess) {
+        st->done = nullptr;
+        return fail(LCFIR_EDEVICE, "event creation failed");
+    }
+    return LCFIR_OK;
+}
 
 std::atomic<int> g_staging_mode{LCFIR_STAGING_PAGEABLE};
 std::atomic<int> g_range_profile{0};
@@ -338,7 +391,25 @@ int ensure_bounce(Staging *st) {
 // Returns with the DMAs queued (the host copies done).
 int h2d_staged(Staging *st, void *dst, const void *src, size_t bytes, bool &staged) {
     staged = false;
-    if (g_staging_mode.load(std::memory_order_relaxed) == LCFIR_STAGING_PAGEABLE || host_pinned(src, bytes)) {
+    st->linked = false;
+    if (host_pinned(src, bytes)) {
+        Link *lk = device_link(st->device);
+        if (!lk) return fail(LCFIR_EDEVICE, "stream creation failed");
+        if (const int rc = ensure_link_events(st)) return rc;
+        // the slot's buffers (stream-ordered allocations on st->stream) are
+        // ready before the link queue writes them; the kernel waits for the copy
+        LCFIR_HIP(hipEventRecord(st->ev_pre, st->stream));
+        {
+            std::lock_guard<std::mutex> g(lk->in_mu);
+            LCFIR_HIP(hipStreamWaitEvent(lk->in, st->ev_pre, 0));
+            LCFIR_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, lk->in));
+            LCFIR_HIP(hipEventRecord(st->ev_in, lk->in));
+        }
+        st->linked = true;
+        LCFIR_HIP(hipStreamWaitEvent(st->stream, st->ev_in, 0));
+        return LCFIR_OK;
+    }
+    if (g_staging_mode.load(std::memory_order_relaxed) == LCFIR_STAGING_PAGEABLE) {
         LCFIR_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st->stream));
         return LCFIR_OK;
     }
@@ -361,7 +432,25 @@ int h2d_staged(Staging *st, void *dst, const void *src, size_t bytes, bool &stag
 // dst holds the bytes (stream order: the DMAs wait for the kernel).  If
 // `tev_end` is set it is recorded after the last DMA.
 int d2h_staged(Staging *st, void *dst, const void *src, size_t bytes, hipEvent_t tev_end) {
-    if (g_staging_mode.load(std::memory_order_relaxed) == LCFIR_STAGING_PAGEABLE || host_pinned(dst, bytes)) {
+    if (host_pinned(dst, bytes)) {
+        Link *lk = device_link(st->device);
+        if (!lk) return fail(LCFIR_EDEVICE, "stream creation failed");
+        if (const int rc = ensure_link_events(st)) return rc;
+        LCFIR_HIP(hipEventRecord(st->ev_k, st->stream));
+        {
+            std::lock_guard<std::mutex> g(lk->out_mu);
+            LCFIR_HIP(hipStreamWaitEvent(lk->out, st->ev_k, 0));
+            LCFIR_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, lk->out));
+            if (tev_end) LCFIR_HIP(hipEventRecord(tev_end, lk->out));
+            LCFIR_HIP(hipEventRecord(st->done, lk->out));
+        }
+        st->linked = true;
+        // the thread sleeps until its copy lands (a polling wait from 16
+        // threads takes the host cores the other calls need to issue theirs)
+        LCFIR_HIP(hipEventSynchronize(st->done));
+        return LCFIR_OK;
+    }
+    if (g_staging_mode.load(std::memory_order_relaxed) == LCFIR_STAGING_PAGEABLE) {
         LCFIR_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st->stream));
         if (tev_end) LCFIR_HIP(hipEventRecord(tev_end, st->stream));
         LCFIR_HIP(hipStreamSynchronize(st->stream));
@@ -414,6 +503,8 @@ void free_staging(Staging *s) {
         if (s->bev[b]) (void)hipEventDestroy(s->bev[b]);
     }
     for (hipEvent_t e : s->tev)
+        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : {s->ev_pre, s->ev_in, s->ev_k, s->done})
         if (e) (void)hipEventDestroy(e);
     delete s;
 }
@@ -785,7 +876,15 @@ int lcfir_apply_range(lcfir_ctx *ctx, const float *x, int64_t n, float *y, int64
             g_stats.d2h_ms += ms[2];
         }
     }
-    if (rc) (void)hipStreamSynchronize(st->stream); // no DMA of this call may still touch the bounce buffers
+    if (rc) {
+        // no DMA of this call may still touch the bounce buffers or the caller's
+        Link *lk = st->linked ? device_link(st->device) : nullptr;
+        if (lk) {
+            (void)hipStreamSynchronize(lk->in);
+            (void)hipStreamSynchronize(lk->out);
+        }
+        (void)hipStreamSynchronize(st->stream);
+    }
     return_staging(st);
     if (!rc && progress) progress(user, (uint64_t)(end - start));
     return rc;

@@ -5,7 +5,8 @@
 # put the library in abvar/NAME.so (git-ignored; gpurun ships it).  The
 # product tree never carries experiment switches;
 # scripts/gpu_run.sh's ab: and parity: steps time and check the variants.
-# usage: bash scripts/build_variant.sh NAME [PATCH]    (no PATCH: the product as NAME)
+# usage: bash scripts/build_variant.sh NAME [PATCH]    (no PATCH: the product as NAME;
+# the patches measured so far are scripts/variants/*.patch, README there)
 # Also builds tools/fft32r_trace from the patched source as abvar/NAME.trace.
 set -euo pipefail
 ROOT="$(cd "$(dirname "$0")/.." && pwd)"

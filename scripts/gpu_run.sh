@@ -19,10 +19,12 @@
 #   pmc[:ARGS]              FETCH_SIZE / WRITE_SIZE / VALU-instruction passes (one
 #                           rocprofv3 --pmc run each) + pmc_summary.json
 #   pmcre:REGEX[:ARGS]      FETCH_SIZE / WRITE_SIZE passes over the kernels matching REGEX
+#   traffic:NTAPS:SPL:KERNEL:SEG[:ARGS]  bench.py's PMC sidecar (traffic.json) for one bench line
 #   tool:NAME[:ARGS]        audio-fir-filter_amd/tools/NAME (a built development tool)
 #   dropin[:ARGS]           tests/cpp/dropin_bench
 #   dropin_nosdma[:ARGS]    the same with HSA_ENABLE_SDMA=0 (copies by blit kernels)
 #   vdropin:V[:ARGS]        the same over variant V's library
+#   dropintrace[:V[:ARGS]]  kernel + memory-copy trace of the pinned drop-in (copy_overlap.py)
 #   gpus2[:ARGS]            bench.py --gpus 2 rehearsal on one device (gloo)
 # Words in ARGS are separated by spaces (quote the whole STEP).
 set -u -o pipefail
@@ -68,7 +70,7 @@ for S in "$@"; do
                 N=$((N + 1)); log="$OUT/${N}_ab_${v}_$rep.log"
                 timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-ingest $args > "$log" 2>&1 \
                     || { echo "!! ab $v failed"; tail -20 "$log"; exit 1; }
-                echo "$v rep$rep $(brief < "$log")" | tee -a "$OUT/ab.txt"
+                echo "$v rep$rep $(brief < "$log") [$args]" | tee -a "$OUT/ab.txt"
             done
         done
         restore ;;
@@ -88,24 +90,46 @@ for S in "$@"; do
         v=${rest%%:*}; args=""; [ "$v" != "$rest" ] && args=${rest#*:}
         run "trace_$v" 120 "abvar/$v.trace" ${args:-4001 32768} ;;
     prof)
-        (cd /tmp && export TMPDIR=/tmp && run prof 600 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof" -o bench -- \
-            python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-parity --no-ingest $rest) || exit 1
-        python3 scripts/trace_exclusive.py "$OUT/prof/bench_kernel_trace.csv" > "$OUT/exclusive_from_trace.json"
-        cat "$OUT/exclusive_from_trace.json" | head -c 600; echo ;;
+        # run() in this shell (not a subshell), so the step counter advances
+        d="$OUT/prof$((N + 1))"
+        cd /tmp; export TMPDIR=/tmp
+        run prof 600 rocprofv3 --kernel-trace --stats -f csv -d "$d" -o bench -- \
+            python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-parity --no-ingest $rest
+        cd "$ROOT"
+        python3 scripts/trace_exclusive.py "$d/bench_kernel_trace.csv" > "$d/exclusive_from_trace.json"
+        head -c 600 "$d/exclusive_from_trace.json"; echo ;;
     pmc|pmcre)
         # pmcre:REGEX[:ARGS] -- the kernels matching REGEX (default 'fir_'), traffic passes only
         re='fir_'; passes=(FETCH_SIZE WRITE_SIZE "SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64")
         if [ "$kind" = pmcre ]; then
             re=${rest%%:*}; r2=""; [ "$re" != "$rest" ] && r2=${rest#*:}; rest=$r2; passes=(FETCH_SIZE WRITE_SIZE)
         fi
-        d="$OUT/$kind$N"; i=0
+        d="$OUT/$kind$((N + 1))"; i=0
+        cd /tmp; export TMPDIR=/tmp
         for c in "${passes[@]}"; do
             i=$((i + 1))
-            (cd /tmp && export TMPDIR=/tmp && run "${kind}_$i" 300 rocprofv3 --pmc $c --kernel-include-regex "$re" -f csv \
+            run "${kind}_$i" 300 rocprofv3 --pmc $c --kernel-include-regex "$re" -f csv \
                 -d "$d/p_$i" -o pmc -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline \
-                --no-parity --no-ingest $rest) || exit 1
+                --no-parity --no-ingest $rest
         done
+        cd "$ROOT"
+        echo "$rest" > "$d/args.txt"
         python3 scripts/pmc_summary.py "$d" --json "$d/pmc_summary.json" > /dev/null && echo "pmc summary ok: $d" ;;
+    traffic) # traffic:NTAPS:SAMPLES_PER_LAUNCH:KERNEL:SEG_LEN[:ARGS] -- the bench's PMC sidecar
+        # (profiles/traffic_*.json: FETCH_SIZE, WRITE_SIZE, f64 VALU passes of the
+        # bench line ARGS names, scripts/make_traffic_json.py over their summary)
+        IFS=: read -r nt spl kern seg targs <<< "$rest"
+        d="$OUT/traffic$((N + 1))"; i=0
+        cd /tmp; export TMPDIR=/tmp
+        for c in FETCH_SIZE WRITE_SIZE "SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64"; do
+            i=$((i + 1))
+            run "traffic_$i" 300 rocprofv3 --pmc $c --kernel-include-regex "$kern" -f csv -d "$d/p_$i" -o pmc -- \
+                python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-parity --no-ingest --ntaps "$nt" ${targs:-}
+        done
+        cd "$ROOT"
+        python3 scripts/pmc_summary.py "$d" --json "$d/pmc_summary.json" > /dev/null &&
+        python3 scripts/make_traffic_json.py "$d/pmc_summary.json" "$d/traffic.json" --method fft --ntaps "$nt" \
+            --samples-per-launch "$spl" --kernel "$kern" --seg-len "$seg" && cat "$d/traffic.json" ;;
     tool) # tool:NAME[:ARGS] -- a development tool under audio-fir-filter_amd/tools
         t=${rest%%:*}; args=""; [ "$t" != "$rest" ] && args=${rest#*:}
         run "tool_$t" 300 "audio-fir-filter_amd/tools/$t" $args ;;
@@ -116,6 +140,16 @@ for S in "$@"; do
         cp "abvar/$v.so" "$LIB"
         run "dropin_$v" 600 tests/cpp/dropin_bench ${args:---threads 1,16,ref --reps 3}
         restore ;;
+    dropintrace) # dropintrace[:V[:ARGS]] -- kernel + memory-copy trace of the pinned 16-thread drop-in
+        # (V: a variant library, default the product), then scripts/copy_overlap.py over it
+        v=${rest%%:*}; args=""; [ "$v" != "$rest" ] && args=${rest#*:}; v=${v:-prod}
+        [ "$v" = prod ] || cp "abvar/$v.so" "$LIB"
+        d="$OUT/dropintrace_$v"
+        cd /tmp; export TMPDIR=/tmp
+        run "dropintrace_$v" 300 rocprofv3 --kernel-trace --memory-copy-trace --hip-trace -f csv -d "$d" -o di -- \
+            "$ROOT/tests/cpp/dropin_bench" ${args:---threads 16 --reps 1 --modes pinned}
+        cd "$ROOT"; restore
+        python3 scripts/copy_overlap.py "$d" | tee "$d/overlap.txt" ;;
     gpus2) LCFIR_BENCH_SHARE_DEVICE=1 run gpus2 400 python bench.py --gpus 2 --steps 10 --warmup 2 $rest ;;
     *) echo "unknown step $S"; exit 2 ;;
     esac

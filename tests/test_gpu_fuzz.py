@@ -25,7 +25,7 @@ switch is sized from the plan itself (lcfir_ctx_fft_units), and every case
 checks which of the two the library took (lcfir_ctx_nrm_stats).
 
 LCFIR_FUZZ_CASES / LCFIR_FUZZ_NORM_CASES / LCFIR_FUZZ_SEED0 widen or shift the
-seed range for a longer campaign (scripts/gpu_fuzz.sh); the defaults are the
+seed range for a longer campaign (scripts/gpu_run.sh fuzz:SEED0,CASES,NORM); the defaults are the
 round-end suite's.
 """
 import os
