@@ -163,8 +163,11 @@ int lcfir_staging_count(int device, int *live, int *idle);
  * buffers; the calling thread copies chunk i into one while the DMA engine
  * moves chunk i - 1 out of the other, both ways (measured slower: 24 GB/s
  * from one thread).  Memory that is already pinned (hipHostMalloc /
- * hipHostRegister) is copied directly in both modes.  Process-wide; takes
- * effect at the next call. */
+ * hipHostRegister) is copied directly in both modes, on one H2D and one D2H
+ * queue per device shared by all calls (the D2H by a kernel through the
+ * buffer's device mapping when both ends are 16-byte aligned), so concurrent
+ * calls use the link both ways at once.  Process-wide; takes effect at the
+ * next call. */
 typedef enum lcfir_staging_mode {
     LCFIR_STAGING_BOUNCE = 0,
     LCFIR_STAGING_PAGEABLE = 1

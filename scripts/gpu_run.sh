@@ -6,7 +6,7 @@
 #
 # usage (repo root, on the GPU box): bash scripts/gpu_run.sh TAG STEP [STEP ...]
 #   smoke                   __graft_entry__.smoke()
-#   suite[:ARGS]            pytest -m gpu (ARGS: extra pytest args, e.g. a file)
+#   suite[:ARGS]            pytest -m gpu over tests/ (ARGS: the files / pytest args instead)
 #   bench[:ARGS]            bench.py --steps 20 --warmup 5 ARGS (the driver's shape)
 #   ab:V1,V2:REPS[:ARGS]    alternating bench lines of abvar/V1.so, abvar/V2.so, ...
 #                           (scripts/build_variant.sh builds them; "prod" = this tree's library)
@@ -60,7 +60,7 @@ for S in "$@"; do
     rest=""; [ "$kind" != "$S" ] && rest=${S#*:}
     case $kind in
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    suite) run suite 1500 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread $rest ;;
+    suite) run suite 1500 python -u -m pytest ${rest:-tests} -m gpu -x -v --timeout 300 --timeout-method thread ;;
     bench) run bench 400 python bench.py --steps 20 --warmup 5 $rest ;;
     ab)
         vs=${rest%%:*}; r2=${rest#*:}; reps=${r2%%:*}; args=""; [ "$r2" != "$reps" ] && args=${r2#*:}

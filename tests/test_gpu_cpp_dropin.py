@@ -201,3 +201,78 @@ def test_apply_range_staging_modes(oracle_mod, mode, ntaps):
     ref, _ = oracle_mod.filter_points(x, taps, idx, oracle_mod.MODE_LD)
     d = want[idx].astype(np.float64) - ref
     assert np.sqrt(np.mean(d * d)) <= 1e-9
+
+
+def test_apply_range_pinned_link_queues(oracle_mod):
+    """Page-locked caller buffers go through the device's two link queues
+    (lcfir.hip `Link`): H2D by the copy engine, D2H by pcie_copy_kernel
+    through the output's device mapping when both ends are 16-byte aligned
+    (else the copy engine).  16 threads calling at once over ranges of every
+    alignment and tail (0..3 floats past a float4), into a hipHostMalloc'd and
+    a hipHostRegister'd output, equal the device call's bytes; the untouched
+    samples around each range stay as they were."""
+    import ctypes
+    import threading
+    import lcfir
+    import synth
+    import torch
+    taps = oracle_mod.design_lowcut(20.0, 48000.0, 4001)
+    n = 2_400_017
+    x = np.ascontiguousarray(synth.file_buffer(1, n, 48000.0, file=32, bits=24)[0])
+    flt = lcfir.Filter(taps)
+    dx = lcfir.DeviceBuffer.from_array(x)
+    dy = lcfir.DeviceBuffer(4 * n)
+    flt.apply_range_dev(dx, n, dy, 0, n)
+    lcfir.sync()
+    want = dy.download(n)
+    lib = lcfir.load()
+    px, py = ctypes.c_void_p(), ctypes.c_void_p()
+    assert lib.lcfir_host_malloc(4 * n, ctypes.byref(px)) == 0
+    assert lib.lcfir_host_malloc(4 * n, ctypes.byref(py)) == 0
+    rt = torch.cuda.cudart()
+    page = 1 << 16
+    raw = np.zeros(n + 2 * page, np.float32)
+    a0 = (-raw.ctypes.data) % page // 4
+    reg = raw[a0:a0 + n]
+    reg_len = (4 * n + page - 1) & ~(page - 1)
+    registered = False
+    try:
+        hx = np.ctypeslib.as_array((ctypes.c_float * n).from_address(px.value))
+        hy = np.ctypeslib.as_array((ctypes.c_float * n).from_address(py.value))
+        hx[:] = x
+        assert int(rt.cudaHostRegister(reg.ctypes.data, reg_len, 0)) == 0
+        registered = True
+        # 16 ranges: starts on and off a float4, lengths with every tail
+        cuts = [0]
+        rng = np.random.default_rng(5)
+        while len(cuts) < 16:
+            cuts.append(cuts[-1] + 150_000 + int(rng.integers(0, 8)))
+        cuts.append(n)
+        ranges = list(zip(cuts[:-1], cuts[1:]))
+        assert {(e - s) % 4 for s, e in ranges} == {0, 1, 2, 3} and {s % 4 for s, _ in ranges} >= {0, 1, 2, 3}
+        for out in (hy, reg):
+            out[:] = 7.0
+            errs = []
+
+            def call(s, e):
+                try:
+                    flt.apply_range(hx, out, s, e)
+                except Exception as ex:  # surfaced below
+                    errs.append(ex)
+            threads = [threading.Thread(target=call, args=r) for r in ranges]
+            for t in threads:
+                t.start()
+            for t in threads:
+                t.join()
+            assert not errs, errs
+            assert np.array_equal(out, want)
+        # a range inside the buffer: its neighbours keep their bytes
+        hy[:] = 7.0
+        flt.apply_range(hx, hy, 1_000_003, 1_000_010)
+        assert np.array_equal(hy[1_000_003:1_000_010], want[1_000_003:1_000_010])
+        assert np.all(hy[:1_000_003] == 7.0) and np.all(hy[1_000_010:] == 7.0)
+    finally:
+        if registered:
+            rt.cudaHostUnregister(reg.ctypes.data)
+        lib.lcfir_host_free(px)
+        lib.lcfir_host_free(py)
