@@ -313,6 +313,11 @@ struct Staging {
 // with 16 calls in flight the runtime's D2H into page-locked memory now and
 // then held its calling thread for ~8 ms and ran at 12.6 GB/s (HIP API +
 // memory-copy trace, profiles/r05_dropin/), which the kernel path does not.
+// Calls moving less than kLinkMinBytes one way keep their copies on their own
+// slot stream: at the reference's default of 179 threads per channel a call is
+// 0.6 MB, and 358 such copies a file one after another on a shared queue cost
+// more in per-copy latency than the link's second direction gives back.
+constexpr size_t kLinkMinBytes = (size_t)2 << 20;
 struct Link {
     std::mutex in_mu, out_mu; // enqueue order = issue order on each queue
     hipStream_t in = nullptr, out = nullptr;
@@ -432,7 +437,8 @@ int ensure_bounce(Staging *st) {
 int h2d_staged(Staging *st, void *dst, const void *src, size_t bytes, bool &staged) {
     staged = false;
     st->linked = false;
-    if (host_pinned(src, bytes)) {
+    const bool pinned = host_pinned(src, bytes);
+    if (pinned && bytes >= kLinkMinBytes) {
         Link *lk = device_link(st->device);
         if (!lk) return fail(LCFIR_EDEVICE, "stream creation failed");
         if (const int rc = ensure_link_events(st)) return rc;
@@ -449,7 +455,7 @@ int h2d_staged(Staging *st, void *dst, const void *src, size_t bytes, bool &stag
         LCFIR_HIP(hipStreamWaitEvent(st->stream, st->ev_in, 0));
         return LCFIR_OK;
     }
-    if (g_staging_mode.load(std::memory_order_relaxed) == LCFIR_STAGING_PAGEABLE) {
+    if (pinned || g_staging_mode.load(std::memory_order_relaxed) == LCFIR_STAGING_PAGEABLE) {
         LCFIR_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st->stream));
         return LCFIR_OK;
     }
@@ -473,7 +479,8 @@ int h2d_staged(Staging *st, void *dst, const void *src, size_t bytes, bool &stag
 // `tev_end` is set it is recorded after the last DMA.
 int d2h_staged(Staging *st, void *dst, const void *src, size_t bytes, hipEvent_t tev_end) {
     void *dmap = nullptr;
-    if (host_pinned(dst, bytes, &dmap)) {
+    const bool pinned = host_pinned(dst, bytes, &dmap);
+    if (pinned && bytes >= kLinkMinBytes) {
         Link *lk = device_link(st->device);
         if (!lk) return fail(LCFIR_EDEVICE, "stream creation failed");
         if (const int rc = ensure_link_events(st)) return rc;
@@ -495,7 +502,7 @@ int d2h_staged(Staging *st, void *dst, const void *src, size_t bytes, hipEvent_t
         LCFIR_HIP(hipEventSynchronize(st->done));
         return LCFIR_OK;
     }
-    if (g_staging_mode.load(std::memory_order_relaxed) == LCFIR_STAGING_PAGEABLE) {
+    if (pinned || g_staging_mode.load(std::memory_order_relaxed) == LCFIR_STAGING_PAGEABLE) {
         LCFIR_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st->stream));
         if (tev_end) LCFIR_HIP(hipEventRecord(tev_end, st->stream));
         LCFIR_HIP(hipStreamSynchronize(st->stream));

@@ -207,17 +207,18 @@ def test_apply_range_pinned_link_queues(oracle_mod):
     """Page-locked caller buffers go through the device's two link queues
     (lcfir.hip `Link`): H2D by the copy engine, D2H by pcie_copy_kernel
     through the output's device mapping when both ends are 16-byte aligned
-    (else the copy engine).  16 threads calling at once over ranges of every
-    alignment and tail (0..3 floats past a float4), into a hipHostMalloc'd and
-    a hipHostRegister'd output, equal the device call's bytes; the untouched
-    samples around each range stay as they were."""
+    (else the copy engine); calls under 2 MiB keep their slot stream.  16
+    threads calling at once over ranges of every alignment and tail (0..3
+    floats past a float4), into a hipHostMalloc'd and a hipHostRegister'd
+    output, equal the device call's bytes; a 7-sample call leaves its
+    neighbours untouched."""
     import ctypes
     import threading
     import lcfir
     import synth
     import torch
     taps = oracle_mod.design_lowcut(20.0, 48000.0, 4001)
-    n = 2_400_017
+    n = 9_600_017  # 16 ranges of >= 2.4 MB: above lcfir.hip's kLinkMinBytes (2 MiB)
     x = np.ascontiguousarray(synth.file_buffer(1, n, 48000.0, file=32, bits=24)[0])
     flt = lcfir.Filter(taps)
     dx = lcfir.DeviceBuffer.from_array(x)
@@ -246,7 +247,7 @@ def test_apply_range_pinned_link_queues(oracle_mod):
         cuts = [0]
         rng = np.random.default_rng(5)
         while len(cuts) < 16:
-            cuts.append(cuts[-1] + 150_000 + int(rng.integers(0, 8)))
+            cuts.append(cuts[-1] + 600_000 + int(rng.integers(0, 8)))
         cuts.append(n)
         ranges = list(zip(cuts[:-1], cuts[1:]))
         assert {(e - s) % 4 for s, e in ranges} == {0, 1, 2, 3} and {s % 4 for s, _ in ranges} >= {0, 1, 2, 3}
