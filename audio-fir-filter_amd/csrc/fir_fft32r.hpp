@@ -425,9 +425,11 @@ __device__ __forceinline__ void r32_bar() {
 // r32_task_word; c8: the special lane's bin-N/2 coefficient (real).
 // kNrm: the launch also rescales a previous file's outputs (FftNrm, as
 // fir_fft_f64_kernel): unit u's slice is two halves, 2u and 2u + 1 of slice / 2
-// floats, which the older waves (0..3) load, rescale and store while they
-// wait at T1's first barrier and at T1 backwards' first barrier (the younger
-// waves arrive there thousands of cycles later).
+// floats, which the older waves (0..3) load, rescale and store one after the
+// other while they wait at T1 backwards' first barrier (the younger waves
+// arrive there thousands of cycles later).  Not at T1's first barrier: there
+// the younger waves are still in the previous unit's memory phase, and a half
+// moved there costs the config-5 step 2-3 % (scripts/variants/nrm_bar1.patch).
 // Probe: phase-boundary hook (R32NoProbe in the product).
 template <int kOut = kFftOutSym, bool kNrm = false, class Probe = R32NoProbe> // templates: host-only users emit no kernel stub
 __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, const double2 *__restrict__ pair,
@@ -519,7 +521,6 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
 #pragma unroll
         for (int i = 0; i < 16; ++i) flds[kR32Rg * w + 64 * i + lane] = a[i];
         Probe::stamp(2, rnd);
-        nrm_half(u, 0, j, wu);
         r32_bar();
         Probe::stamp(3, rnd);
         if (pk_pending >= 0) {
@@ -704,6 +705,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
 #pragma unroll
         for (int i = 0; i < 16; ++i) flds[kR32Rg * w + 64 * i + lane] = c[i];
         Probe::stamp(16, rnd);
+        nrm_half(u, 0, j, wu);
         nrm_half(u, 1, j, wu);
         r32_bar();
         Probe::stamp(17, rnd);
