@@ -299,11 +299,14 @@ __device__ __forceinline__ void r32_dma_part(const DirectParams &p, int ch, int6
     const int64_t w0 = n0 - p.half - p.x_lo;
     const int vofs = 4096 * (lane >> 5) + 512 * w + 16 * (lane & 31);
     const int sofs = (int)(w0 * 4);
+    // one address-space cast of the array base, the region offset in bytes
+    // (casting each element pointer miscompiles in some instantiations)
+    const uint32_t lds0 = (uint32_t)(size_t)(fft_lds_void *)flds;
 #pragma unroll
     for (int s = s0; s < s1; ++s)
         r32_dma_asm(x, (uint32_t)((p.x_hi - p.x_lo) * 4),
-                    __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(fft_lds_void *)(flds + kR32Rg * w + 64 * s)),
-                    vofs, sofs + 8192 * s);
+                    __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)(16 * (kR32Rg * w + 64 * s))), vofs,
+                    sofs + 8192 * s);
 }
 __device__ __forceinline__ void r32_stage_samples(const DirectParams &p, int ch, int64_t n0, int j, double2 *flds) {
     const int w = j >> 6, lane = j & 63;
@@ -491,8 +494,10 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
         const int64_t n0 = p.seg0 + (int64_t)(u - ch * gd.nseg) * B;
         double2 a[32];
         // the staging transfers have landed; the previous unit's pair stores
-        // (issued after them) may still be in flight
+        // (issued after them) may still be in flight.  The older waves issued
+        // the younger waves' transfers too: everyone waits for their waits.
         __builtin_amdgcn_s_waitcnt(r32_vmcnt(kR32PairStores));
+        r32_bar();
         Probe::stamp(0, rnd);
         // ---- stage 1: the samples out of the wave's region (staged by the
         // previous unit), waves 4..7 negating the odd ones; DFT32; W_16384^(b k1)
@@ -736,6 +741,7 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
         // the compiler's vmcnt accounting ignores LDS-DMA; see fir_fft32.hpp)
         {
             __builtin_amdgcn_s_waitcnt(0x0070);
+            r32_bar(); // every wave's reads of its region have returned
             const int un1 = fft_unit32(rnd + 1, blockIdx.x, gridDim.x, gd.units);
             const int un = un1 < gd.units ? un1 : u;
             const int cn = fft_div(un, gd);
@@ -745,12 +751,17 @@ __global__ __launch_bounds__(kFftNT) void fir_fft32r_kernel(DirectParams p, cons
             Probe::stamp(22, rnd);
             // ---- final: * W_16384^(b k1), DFT32 over k1 -> n (an interior next
             // unit's DMA issued in quarters between the VALU blocks, so a wave
-            // whose transfer waits for the CU's memory queue still computes)
+            // whose transfer waits for the CU's memory queue still computes).
+            // The older waves (0..3) issue every region's transfers, theirs and
+            // wave + 4's: the younger waves, which leave the final phase last
+            // (their VALU issues second), then only compute and store
+            // (config 2 launch -6 %, config 4 -5 %, scripts/variants/README.md)
             auto part = [&](auto q) {
                 constexpr int k = decltype(q)::value;
-                if (split) {
+                if (split && !hi) {
                     __builtin_amdgcn_sched_barrier(0);
                     r32_dma_part<4 * k, 4 * k + 4>(p, cn, nn, j, flds);
+                    r32_dma_part<4 * k, 4 * k + 4>(p, cn, nn, j + 256, flds);
                     __builtin_amdgcn_sched_barrier(0);
                 }
             };
