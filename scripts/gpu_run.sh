@@ -19,6 +19,7 @@
 #   pmc[:ARGS]              FETCH_SIZE / WRITE_SIZE / VALU-instruction passes (one
 #                           rocprofv3 --pmc run each) + pmc_summary.json
 #   pmcre:REGEX[:ARGS]      FETCH_SIZE / WRITE_SIZE passes over the kernels matching REGEX
+#   pmcx:C1,C2,..:REGEX[:ARGS]  one --pmc pass of those counters (per-block limits apply)
 #   traffic:NTAPS:SPL:KERNEL:SEG[:ARGS]  bench.py's PMC sidecar (traffic.json) for one bench line
 #   tool:NAME[:ARGS]        audio-fir-filter_amd/tools/NAME (a built development tool)
 #   dropin[:ARGS]           tests/cpp/dropin_bench
@@ -115,6 +116,15 @@ for S in "$@"; do
         cd "$ROOT"
         echo "$rest" > "$d/args.txt"
         python3 scripts/pmc_summary.py "$d" --json "$d/pmc_summary.json" > /dev/null && echo "pmc summary ok: $d" ;;
+    pmcx) # pmcx:COUNTERS:REGEX[:ARGS] -- one --pmc pass of the given counters (comma-separated;
+        # within rocprofv3's per-block limits) over the kernels matching REGEX
+        IFS=: read -r cl re targs <<< "$rest"
+        d="$OUT/pmcx$((N + 1))"
+        cd /tmp; export TMPDIR=/tmp
+        run pmcx 300 rocprofv3 --pmc ${cl//,/ } --kernel-include-regex "$re" -f csv -d "$d/p_1" -o pmc -- \
+            python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-parity --no-ingest ${targs:-}
+        cd "$ROOT"
+        python3 scripts/pmc_summary.py "$d" --json "$d/pmc_summary.json" > /dev/null && cat "$d/pmc_summary.json" ;;
     traffic) # traffic:NTAPS:SAMPLES_PER_LAUNCH:KERNEL:SEG_LEN[:ARGS] -- the bench's PMC sidecar
         # (profiles/traffic_*.json: FETCH_SIZE, WRITE_SIZE, f64 VALU passes of the
         # bench line ARGS names, scripts/make_traffic_json.py over their summary)
