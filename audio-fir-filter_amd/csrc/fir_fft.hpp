@@ -216,9 +216,12 @@ inline int fft_partition_count(int ntaps, int L = 16384) {
 // from ~4 000 taps (config 2's 4 001: 7.65e-5 against 8.07e-5 per output).
 constexpr double kFft32rUnitCost = 2.2;
 // Zero-phase single-partition L = 16384 plans run fir_fft16r_kernel (two
-// 256-thread workgroups per CU, the transform in registers): its unit cost
-// per CU, relative to one fir_fft_f64_kernel unit.
-constexpr double kFft16rUnitCost = 0.65;
+// 256-thread workgroups per CU, the transform in registers) in the register
+// family: its unit cost per CU, relative to one fir_fft_f64_kernel unit, as
+// measured in round 5 against fir_fft32r (0.93 on config 2, 1.06 on config 4's
+// long file) -- the design estimate of 0.65 sent the
+// family's 4 001-tap plans to L = 16 384, where the kernel is slower.
+constexpr double kFft16rUnitCost = 1.0;
 // FftTuning::family: the default takes fir_fft32r at L = 32 768 and the
 // LDS-column kernel at L = 16 384; kFamilyRegister adds fir_fft16r at 16 384
 constexpr int kFamilyDefault = 0, kFamilyLds = 1, kFamilyRegister = 2;

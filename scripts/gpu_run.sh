@@ -11,7 +11,7 @@
 #   ab:V1,V2:REPS[:ARGS]    alternating bench lines of abvar/V1.so, abvar/V2.so, ...
 #                           (scripts/build_variant.sh builds them; "prod" = this tree's library)
 #   parity:V[:ARGS]         the FFT parity + fuzz tests with abvar/V.so in place
-#   fuzz:SEED0,CASES,NORM   seeded fuzz campaign (tests/test_gpu_fuzz.py)
+#   fuzz:SEED0,CASES,NORM[,FAMILY]  seeded fuzz campaign (tests/test_gpu_fuzz.py; FAMILY: lds, register)
 #   trace[:ARGS]            tools/fft32r_trace phase timeline (default 4001 32768)
 #   vtrace:V[:ARGS]         the same tool built from variant V's source (abvar/V.trace)
 #   prof[:ARGS]             rocprofv3 --kernel-trace --stats of a bench line + the
@@ -82,8 +82,8 @@ for S in "$@"; do
             tests/test_gpu_parity.py tests/test_gpu_fuzz.py tests/test_gpu_baseline_configs.py $args
         restore ;;
     fuzz)
-        IFS=, read -r s0 nc nn <<< "$rest"
-        LCFIR_FUZZ_SEED0=$s0 LCFIR_FUZZ_CASES=$nc LCFIR_FUZZ_NORM_CASES=$nn \
+        IFS=, read -r s0 nc nn fam <<< "$rest"
+        LCFIR_FUZZ_SEED0=$s0 LCFIR_FUZZ_CASES=$nc LCFIR_FUZZ_NORM_CASES=$nn LCFIR_FUZZ_FAMILY=${fam:-default} \
             run fuzz 900 python -u -m pytest tests/test_gpu_fuzz.py -m gpu -q -p no:cacheprovider \
             --timeout 120 --timeout-method thread ;;
     trace) run trace 120 audio-fir-filter_amd/tools/fft32r_trace ${rest:-4001 32768} ;;

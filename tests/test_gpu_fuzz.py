@@ -25,8 +25,11 @@ switch is sized from the plan itself (lcfir_ctx_fft_units), and every case
 checks which of the two the library took (lcfir_ctx_nrm_stats).
 
 LCFIR_FUZZ_CASES / LCFIR_FUZZ_NORM_CASES / LCFIR_FUZZ_SEED0 widen or shift the
-seed range for a longer campaign (scripts/gpu_run.sh fuzz:SEED0,CASES,NORM); the defaults are the
-round-end suite's.
+seed range for a longer campaign (scripts/gpu_run.sh fuzz:SEED0,CASES,NORM[,FAMILY]); the defaults are the
+round-end suite's.  LCFIR_FUZZ_FAMILY (lcfir_ctx_set_fft_family: default, lds,
+register) runs the FFT cases on another kernel family: "register" puts the
+L = 16 384 zero-phase cases on fir_fft16r_kernel, "lds" the L = 32 768 ones on
+the park-slab kernel.
 """
 import os
 
@@ -39,6 +42,7 @@ RMS_TOL = 1e-9
 SEED0 = int(os.environ.get("LCFIR_FUZZ_SEED0", "0"))
 N_CASES = int(os.environ.get("LCFIR_FUZZ_CASES", "120"))
 N_NORM_CASES = int(os.environ.get("LCFIR_FUZZ_NORM_CASES", "40"))
+FAMILY = os.environ.get("LCFIR_FUZZ_FAMILY", "default")
 
 
 def _max_ulps(a, b, floor=1e-12):
@@ -88,6 +92,8 @@ def test_random_case(oracle_mod, seed):
     flt = lc.Filter(taps, method=method)
     if method == "fft" and _seg32(seed):
         flt.set_fft_tuning(seg_len=32768)
+    if method == "fft" and FAMILY != "default":
+        flt.set_fft_family(FAMILY)
 
     dx = lc.DeviceBuffer.from_array(x)
     dy = lc.DeviceBuffer(x.nbytes)
@@ -199,8 +205,10 @@ def test_random_norm_case(oracle_mod, seed):
     flt = lc.Filter(taps, method=method)
     if method == "fft" and _seg32(seed):
         flt.set_fft_tuning(seg_len=32768)
+    if method == "fft" and FAMILY != "default":
+        flt.set_fft_family(FAMILY)
     units = flt.fft_units
-    if method == "fft" and designed and ntaps >= 4001:
+    if method == "fft" and designed and ntaps >= 4001 and FAMILY != "lds":
         # linear-phase filters from ~4 000 taps run the register kernel
         assert units["kernel"] == "l32_reg", (seed, units)
     count, offset, peaks, force, want_fused = _norm_params(rng, n, nch, units)
