@@ -321,9 +321,10 @@ constexpr size_t kLinkMinBytes = (size_t)2 << 20;
 struct Link {
     std::mutex in_mu, out_mu; // enqueue order = issue order on each queue
     hipStream_t in = nullptr, out = nullptr;
+    int device = 0;
 };
-std::mutex g_link_mu;
-std::vector<Link *> g_links; // per device, created on first use, never destroyed
+std::mutex g_link_mu; // taken after g_pool_mu where both are held
+std::vector<Link *> g_links; // per device, created on first use; lcfir_staging_release frees them
 
 Link *device_link(int device) {
     std::lock_guard<std::mutex> lk(g_link_mu);
@@ -331,6 +332,7 @@ Link *device_link(int device) {
     Link *&l = g_links[(size_t)device];
     if (!l) {
         auto *n = new Link;
+        n->device = device;
         if (hipStreamCreateWithFlags(&n->in, hipStreamNonBlocking) != hipSuccess ||
             hipStreamCreateWithFlags(&n->out, hipStreamNonBlocking) != hipSuccess) {
             if (n->in) (void)hipStreamDestroy(n->in);
@@ -964,6 +966,7 @@ int lcfir_range_stats_get(lcfir_range_stats *out, int reset) {
 
 int lcfir_staging_release(int device) {
     std::vector<Staging *> idle;
+    std::vector<Link *> links;
     {
         std::lock_guard<std::mutex> lk(g_pool_mu);
         for (size_t i = 0; i < g_pool.size();) {
@@ -975,9 +978,27 @@ int lcfir_staging_release(int device) {
                 ++i;
             }
         }
+        // a device left with no slot has no call in flight (a call holds its
+        // slot throughout), and none can start while g_pool_mu is held: its
+        // link queues go too (the next pinned call creates them again)
+        std::lock_guard<std::mutex> lk2(g_link_mu);
+        for (size_t d = 0; d < g_links.size(); ++d)
+            if (g_links[d] && (device < 0 || (int)d == device) &&
+                (d >= g_pool_live.size() || g_pool_live[d] == 0)) {
+                links.push_back(g_links[d]);
+                g_links[d] = nullptr;
+            }
     }
     g_pool_cv.notify_all();
     for (Staging *st : idle) free_staging(st);
+    for (Link *l : links) {
+        DeviceGuard g(l->device);
+        (void)hipStreamSynchronize(l->in);
+        (void)hipStreamSynchronize(l->out);
+        (void)hipStreamDestroy(l->in);
+        (void)hipStreamDestroy(l->out);
+        delete l;
+    }
     return LCFIR_OK;
 }
 

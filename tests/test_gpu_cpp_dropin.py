@@ -272,6 +272,13 @@ def test_apply_range_pinned_link_queues(oracle_mod):
         flt.apply_range(hx, hy, 1_000_003, 1_000_010)
         assert np.array_equal(hy[1_000_003:1_000_010], want[1_000_003:1_000_010])
         assert np.all(hy[:1_000_003] == 7.0) and np.all(hy[1_000_010:] == 7.0)
+        # releasing every slot releases the device's link queues too; the
+        # next pinned call builds them again
+        lcfir.staging_release(0)
+        assert lcfir.staging_count(0) == (0, 0)
+        hy[:] = 7.0
+        flt.apply_range(hx, hy, 0, n)
+        assert np.array_equal(hy, want)
     finally:
         if registered:
             rt.cudaHostUnregister(reg.ctypes.data)
