@@ -152,7 +152,8 @@ int lcfir_apply_range(lcfir_ctx *ctx, const float *x, int64_t n, float *y, int64
  * buffers) per call from a per-device pool of at most 16 slots; callers beyond
  * that wait for a free slot, so the reference's default of floor(0.7 cores)
  * threads per channel (main.cp:75) never creates a stream per thread.
- * lcfir_staging_release frees the idle slots of `device` (-1: every device);
+ * lcfir_staging_release frees the idle slots of `device` (-1: every device),
+ * and a device's two link queues (page-locked copies) once it has no slot left;
  * lcfir_staging_count reports the slots in existence and the idle ones. */
 int lcfir_staging_release(int device);
 int lcfir_staging_count(int device, int *live, int *idle);
