@@ -132,8 +132,7 @@ struct FftTuning {
     int64_t chunk = 0;      // outputs per launch chunk; 0 = 2^28 (the buffer offsets' 32-bit range)
     int64_t max_units = 0;  // units per launch; 0 = 2^31 - 1 (FftGrid's 32-bit unit index)
     // kernel family of zero-phase single-partition plans (lcfir_ctx_set_fft_family):
-    // kFamilyDefault, kFamilyLds (the LDS-column kernels everywhere) or
-    // kFamilyRegister (the register-resident kernel of either segment length)
+    // kFamilyDefault or kFamilyLds (the LDS-column kernels everywhere)
     int32_t family = 0;
 };
 
@@ -154,7 +153,6 @@ struct FftPlan {
     int cus = 256;             // compute units of the plan's device (persistent grid)
     bool sym = false;          // linear-phase filter run in zero-phase form (kFftOutSym)
     bool reg32 = false;        // L = 32768 zero-phase on the register-resident kernel (fir_fft32r.hpp)
-    bool reg16 = false;        // L = 16384 zero-phase on the two-workgroups-per-CU register kernel (fir_fft16r.hpp)
     FftTuning tune;            // the ctx's tuning when the plan was built
 };
 
@@ -215,24 +213,16 @@ inline int fft_partition_count(int ntaps, int L = 16384) {
 // persistent-grid round), so it takes linear-phase filters
 // from ~4 000 taps (config 2's 4 001: 7.65e-5 against 8.07e-5 per output).
 constexpr double kFft32rUnitCost = 2.2;
-// Zero-phase single-partition L = 16384 plans run fir_fft16r_kernel (two
-// 256-thread workgroups per CU, the transform in registers) in the register
-// family: its unit cost per CU, relative to one fir_fft_f64_kernel unit, as
-// measured in round 5 against fir_fft32r (0.93 on config 2, 1.06 on config 4's
-// long file) -- the design estimate of 0.65 sent the
-// family's 4 001-tap plans to L = 16 384, where the kernel is slower.
-constexpr double kFft16rUnitCost = 1.0;
 // FftTuning::family: the default takes fir_fft32r at L = 32 768 and the
-// LDS-column kernel at L = 16 384; kFamilyRegister adds fir_fft16r at 16 384
-constexpr int kFamilyDefault = 0, kFamilyLds = 1, kFamilyRegister = 2;
+// LDS-column kernel at L = 16 384; kFamilyLds the LDS-column kernels at both.
+// (Family 2, round 5's L = 16 384 two-workgroups-per-CU register kernel, is a
+// variant patch now: scripts/variants/r16_kernel.patch, not faster on any
+// config.)
+constexpr int kFamilyDefault = 0, kFamilyLds = 1;
 inline bool fft_reg32(int L, int parts, bool sym, const FftTuning &tune = FftTuning{}) {
     return L == 32768 && parts == 1 && sym && tune.family != kFamilyLds;
 }
-inline bool fft_reg16(int L, int parts, bool sym, const FftTuning &tune = FftTuning{}) {
-    return L == 16384 && parts == 1 && sym && tune.family == kFamilyRegister;
-}
 inline double fft_unit_cost(int L, int parts, bool sym, const FftTuning &tune = FftTuning{}) {
-    if (fft_reg16(L, parts, sym, tune)) return kFft16rUnitCost;
     if (L == 16384) return parts == 1 ? 1.0 : 1.25;
     if (fft_reg32(L, parts, sym, tune)) return kFft32rUnitCost;
     return parts == 1 ? (sym ? 2.9 : 3.1) : 4.0;
@@ -1269,7 +1259,6 @@ __global__ __launch_bounds__(kFftNT) void fir_fft_f64_kernel(DirectParams p, con
 
 #include "fir_fft32.hpp"
 #include "fir_fft32r.hpp"
-#include "fir_fft16r.hpp"
 
 // ---------------------------------------------------------------------------
 // host side
@@ -1314,7 +1303,7 @@ inline void fft_ld(std::vector<long double> &re, std::vector<long double> &im) {
 // test that runs scripts/fft32_model.py's emulation of the kernel on them.
 struct FftTables {
     int L = 0, halves = 1, parts = 1, tp = 0;
-    bool sym = false, reg32 = false, reg16 = false;
+    bool sym = false, reg32 = false;
     std::vector<double2> pair; // parts x halves x kFftPairTable
     std::vector<uint32_t> task; // halves x 512
     std::vector<double2> c8;   // per partition
@@ -1390,73 +1379,6 @@ inline void r32_plan_tables(const std::vector<double> &taps, FftTables &T) {
     T.reg32 = true;
 }
 
-// fir_fft16r_kernel's tables (zero-phase, one partition, L = 16384): per
-// thread t and pair slot i the zero-phase coefficients p1, q2, p2 of the bin in
-// its R1 register i (the special lane: of its permuted x' list), the task
-// words, and the twiddles W_8192^b (b < 256), W_256^g (g < 16).
-inline void r16_plan_tables(const std::vector<double> &taps, FftTables &T) {
-    const int ntaps = (int)taps.size(), L = kR16L, N = L / 2;
-    const long double scale = 1.0L / (4.0L * (long double)N);
-    const long double two_pi = 6.283185307179586476925286766559L;
-    std::vector<long double> re((size_t)L, 0.0L), im((size_t)L, 0.0L);
-    const int half = (ntaps - 1) / 2;
-    for (int j = -half; j <= half; ++j)
-        re[(size_t)((j + L) % L)] =
-            ((long double)taps[(size_t)(half + j)] + (long double)taps[(size_t)(half - j)]) * 0.5L;
-    detail::fft_ld(re, im);
-    auto coef = [&](int k, long double &p1, long double &q2, long double &p2, long double &c8v) {
-        const long double gr = re[(size_t)k] * scale, hr = re[(size_t)(N - k)] * scale;
-        const long double sr = gr + hr, dr = gr - hr;
-        const long double a = -two_pi * (long double)k / (long double)L;
-        p1 = 2 * sr + 2 * dr * sinl(a);
-        q2 = 2 * sr - 2 * dr * sinl(a);
-        p2 = 2 * dr * cosl(a);
-        c8v = 2 * sr - 2 * dr;
-    };
-    T.pair.assign(kR16PairTable, make_double2(0.0, 0.0));
-    T.task.resize(kR16NT);
-    for (int t = 0; t < kR16NT; ++t) {
-        T.task[(size_t)t] = r16_task_word(t);
-        int bx[16], by[16];
-        r16_task_bins(t, bx, by);
-        if (t == kR16SpecialLane) {
-            // x' = [R2 0..7, R1 1..7, R1 0] (fir_fft16r_kernel's permutation)
-            int px[16];
-            for (int i = 0; i < 8; ++i) px[i] = by[i];
-            for (int i = 8; i < 15; ++i) px[i] = bx[i - 7];
-            px[15] = bx[0];
-            for (int i = 0; i < 16; ++i) bx[i] = px[i];
-        }
-        for (int i = 0; i < 16; ++i) {
-            long double p1, q2, p2, c8v;
-            coef(bx[i], p1, q2, p2, c8v);
-            T.pair[(size_t)i * kR16NT + (size_t)t] = make_double2((double)p1, (double)q2);
-            double *p2t = reinterpret_cast<double *>(&T.pair[(size_t)(16 + (i >> 1)) * kR16NT + (size_t)t]);
-            p2t[i & 1] = (double)p2;
-        }
-    }
-    {
-        long double p1, q2, p2, c8v;
-        coef(N / 2, p1, q2, p2, c8v);
-        T.c8.assign(1, make_double2((double)c8v, 0.0));
-    }
-    T.tw.resize(kR16Tw);
-    for (int b = 0; b < 256; ++b) {
-        const long double a = -two_pi * (long double)b / 8192.0L;
-        T.tw[(size_t)(kR16TwB + b)] = make_double2((double)cosl(a), (double)sinl(a));
-    }
-    for (int g = 0; g < 16; ++g) {
-        const long double a = -two_pi * (long double)g / 256.0L;
-        T.tw[(size_t)(kR16TwG + g)] = make_double2((double)cosl(a), (double)sinl(a));
-    }
-    T.L = L;
-    T.halves = 1;
-    T.parts = 1;
-    T.tp = ntaps;
-    T.sym = true;
-    T.reg16 = true;
-}
-
 inline FftTables fft_plan_tables(const std::vector<double> &taps, const FftTuning &tune) {
     const int ntaps = (int)taps.size();
     // segment length: the tuning's, else the filter's cheaper one per output;
@@ -1481,10 +1403,6 @@ inline FftTables fft_plan_tables(const std::vector<double> &taps, const FftTunin
     std::vector<uint32_t> &task = T.task;
     if (fft_reg32(L, parts, sym, tune)) {
         r32_plan_tables(taps, T);
-        return T;
-    }
-    if (fft_reg16(L, parts, sym, tune)) {
-        r16_plan_tables(taps, T);
         return T;
     }
     pair.resize((size_t)parts * halves * kFftPairTable);
@@ -1616,7 +1534,6 @@ inline bool fft_plan_build(FftPlan &plan, const double *d_taps, int ntaps, const
     plan.parts = T.parts;
     plan.sym = T.sym;
     plan.reg32 = T.reg32;
-    plan.reg16 = T.reg16;
     plan.tune = tune;
     plan.B = T.L - T.tp + 1;
     plan.c8 = T.c8;
@@ -1642,36 +1559,6 @@ inline int64_t fft_chunk(const FftPlan &plan) {
 
 // work array + twiddles + 8 f32 peak slots + the special lane's 32 double2
 constexpr size_t kR32LdsBytes = sizeof(double2) * (size_t)(kR32Work + kR32Tw + 2 + 32);
-
-template <int kOut, bool kNrm = false, class Probe = R32NoProbe>
-inline bool fft16r_launch_one(const FftPlan &plan, const DirectParams &q, int nch, hipStream_t s, std::string &err,
-                              FftNrm nrm = FftNrm{}) {
-    static const bool attr = [] {
-        return hipFuncSetAttribute(reinterpret_cast<const void *>(&fir_fft16r_kernel<kOut, kNrm, Probe>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kR16LdsBytes) == hipSuccess;
-    }();
-    (void)attr;
-    const int64_t nseg = (q.end - q.seg0 + plan.B - 1) / plan.B;
-    const int64_t units = nseg * nch; // < 2^31 (fft_launch)
-    const int64_t grid = std::min<int64_t>(units, (int64_t)kR16WgPerCu * plan.cus);
-    if constexpr (kNrm) {
-        // whole 1 024-float blocks per unit, at most kNrmK16 (fft_nrm_fusable)
-        const int64_t per = (nrm.count + units - 1) / units;
-        nrm.slice = (per + 1023) / 1024 * 1024;
-        if (nrm.slice > (int64_t)kNrmK16 * 1024) {
-            err = "normalize slice too large to fuse";
-            return false;
-        }
-    }
-    hipLaunchKernelGGL((fir_fft16r_kernel<kOut, kNrm, Probe>), dim3((unsigned)grid), dim3(kR16NT), kR16LdsBytes, s,
-                       q, plan.d_pair, plan.d_tw, plan.d_task, plan.B, fft_grid(nseg, units), plan.c8[0].x, nrm);
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) {
-        err = hipGetErrorString(e);
-        return false;
-    }
-    return true;
-}
 
 // Probe: fir_fft32r_kernel's phase hook (tools/fft32r_trace.hip passes its own)
 template <int kOut, bool kNrm = false, class Probe = R32NoProbe>
@@ -1738,11 +1625,6 @@ inline bool fft_launch_one(const FftPlan &plan, const DirectParams &q, int part,
                            std::string &err, FftNrm nrm = FftNrm{}) {
     if constexpr (kOut == kFftOutSym)
         if (plan.reg32) return fft32r_launch_one<kOut, kNrm>(plan, q, nch, s, err, nrm);
-    if (plan.reg16) {
-        if constexpr (kOut == kFftOutSym) return fft16r_launch_one<kOut, kNrm>(plan, q, nch, s, err, nrm);
-        err = "fir_fft16r_kernel runs zero-phase filters only";
-        return false;
-    }
     if constexpr (!kNrm)
         if (plan.L == kFft32L) return fft32_launch_one<kOut>(plan, q, part, nch, s, err);
     static const bool attr = [] {
@@ -1849,7 +1731,6 @@ inline bool fft_launch_group(const FftPlan &plan, const DirectParams &p, int nch
 // from it).
 inline int64_t fft_nrm_unit_floats(const FftPlan &plan) {
     if (plan.parts != 1) return 0;
-    if (plan.reg16) return (int64_t)kNrmK16 * 1024;
     if (plan.reg32) return (int64_t)kNrmK32 * 2048;
     return plan.L == kFftL ? (int64_t)kNrmK * 1024 : 0;
 }

@@ -292,7 +292,10 @@ struct Staging {
     size_t y_cap = 0;
     void *h_bounce[2] = {nullptr, nullptr}; // pinned, kBounceBytes each (lazily)
     hipEvent_t bev[2] = {nullptr, nullptr}; // the last DMA touching h_bounce[b] is done
-    hipEvent_t tev[4] = {};                 // lcfir_range_profile: H2D start/end, kernel end, D2H end
+    // lcfir_range_profile: H2D start / end, kernel end, D2H start / end, each
+    // recorded on the queue that runs that step (the link queues on the link
+    // path), so the copy spans exclude the wait behind other calls' copies
+    hipEvent_t tev[5] = {};
     // link path (pinned caller buffers): slot stream ready / H2D landed /
     // kernel done, and the blocking-sync end of the call
     hipEvent_t ev_pre = nullptr, ev_in = nullptr, ev_k = nullptr, done = nullptr;
@@ -367,9 +370,12 @@ lcfir_range_stats g_stats{};
 // the two ends would accept a range that starts in one registration, ends in
 // another and is pageable in between (hipMemcpyAsync resolves the allocation
 // from the start pointer); such a range is treated as pageable.
-// dev (optional): the range's address in the device's mapping of that
-// allocation (null if it has none)
-bool host_pinned(const void *p, size_t bytes, void **dev = nullptr) {
+// dev (optional): the range's address in `device`'s mapping of that
+// allocation -- null if it has none, or if the allocation was made or
+// registered while another device was current (the caller then copies with
+// hipMemcpyAsync, which resolves any host allocation, instead of writing
+// through a mapping the device may not have)
+bool host_pinned(const void *p, size_t bytes, void **dev = nullptr, int device = -1) {
     hipPointerAttribute_t a{};
     if (hipPointerGetAttributes(&a, p) != hipSuccess || a.type != hipMemoryTypeHost) {
         (void)hipGetLastError();
@@ -385,7 +391,9 @@ bool host_pinned(const void *p, size_t bytes, void **dev = nullptr) {
     if (!(q >= b && bytes <= size && q - b <= size - bytes)) return false;
     if (dev) {
         void *db = nullptr;
-        if (hipHostGetDevicePointer(&db, reinterpret_cast<void *>(b), 0) != hipSuccess || !db) {
+        if (a.device != device) {
+            *dev = nullptr;
+        } else if (hipHostGetDevicePointer(&db, reinterpret_cast<void *>(b), 0) != hipSuccess || !db) {
             (void)hipGetLastError();
             *dev = nullptr;
         } else {
@@ -435,8 +443,9 @@ int ensure_bounce(Staging *st) {
 
 // Host -> device on the slot's stream.  Pageable source in bounce mode: chunk
 // i is copied into bounce i mod 2 once the DMA of chunk i - 2 has left it.
-// Returns with the DMAs queued (the host copies done).
-int h2d_staged(Staging *st, void *dst, const void *src, size_t bytes, bool &staged) {
+// Returns with the DMAs queued (the host copies done).  tev (optional): its
+// [0] and [1] are recorded around the copies on the queue that runs them.
+int h2d_staged(Staging *st, void *dst, const void *src, size_t bytes, bool &staged, hipEvent_t *tev = nullptr) {
     staged = false;
     st->linked = false;
     const bool pinned = host_pinned(src, bytes);
@@ -450,15 +459,19 @@ int h2d_staged(Staging *st, void *dst, const void *src, size_t bytes, bool &stag
         {
             std::lock_guard<std::mutex> g(lk->in_mu);
             LCFIR_HIP(hipStreamWaitEvent(lk->in, st->ev_pre, 0));
+            if (tev) LCFIR_HIP(hipEventRecord(tev[0], lk->in));
             LCFIR_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, lk->in));
+            if (tev) LCFIR_HIP(hipEventRecord(tev[1], lk->in));
             LCFIR_HIP(hipEventRecord(st->ev_in, lk->in));
         }
         st->linked = true;
         LCFIR_HIP(hipStreamWaitEvent(st->stream, st->ev_in, 0));
         return LCFIR_OK;
     }
+    if (tev) LCFIR_HIP(hipEventRecord(tev[0], st->stream));
     if (pinned || g_staging_mode.load(std::memory_order_relaxed) == LCFIR_STAGING_PAGEABLE) {
         LCFIR_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st->stream));
+        if (tev) LCFIR_HIP(hipEventRecord(tev[1], st->stream));
         return LCFIR_OK;
     }
     if (const int rc = ensure_bounce(st)) return rc;
@@ -473,15 +486,17 @@ int h2d_staged(Staging *st, void *dst, const void *src, size_t bytes, bool &stag
         LCFIR_HIP(hipMemcpyAsync(d + off, st->h_bounce[b], len, hipMemcpyHostToDevice, st->stream));
         LCFIR_HIP(hipEventRecord(st->bev[b], st->stream));
     }
+    if (tev) LCFIR_HIP(hipEventRecord(tev[1], st->stream));
     return LCFIR_OK;
 }
 
 // Device -> host after the work queued on the slot's stream; returns once
-// dst holds the bytes (stream order: the DMAs wait for the kernel).  If
-// `tev_end` is set it is recorded after the last DMA.
-int d2h_staged(Staging *st, void *dst, const void *src, size_t bytes, hipEvent_t tev_end) {
+// dst holds the bytes (stream order: the DMAs wait for the kernel).  tev
+// (optional): its [3] and [4] are recorded around the copies on the queue
+// that runs them.
+int d2h_staged(Staging *st, void *dst, const void *src, size_t bytes, hipEvent_t *tev = nullptr) {
     void *dmap = nullptr;
-    const bool pinned = host_pinned(dst, bytes, &dmap);
+    const bool pinned = host_pinned(dst, bytes, &dmap, st->device);
     if (pinned && bytes >= kLinkMinBytes) {
         Link *lk = device_link(st->device);
         if (!lk) return fail(LCFIR_EDEVICE, "stream creation failed");
@@ -490,12 +505,13 @@ int d2h_staged(Staging *st, void *dst, const void *src, size_t bytes, hipEvent_t
         {
             std::lock_guard<std::mutex> g(lk->out_mu);
             LCFIR_HIP(hipStreamWaitEvent(lk->out, st->ev_k, 0));
+            if (tev) LCFIR_HIP(hipEventRecord(tev[3], lk->out));
             if (dmap && pcie_copy_fits(dmap, src, bytes)) {
                 if (const int rc = pcie_copy(dmap, src, bytes, lk->out)) return rc;
             } else {
                 LCFIR_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, lk->out));
             }
-            if (tev_end) LCFIR_HIP(hipEventRecord(tev_end, lk->out));
+            if (tev) LCFIR_HIP(hipEventRecord(tev[4], lk->out));
             LCFIR_HIP(hipEventRecord(st->done, lk->out));
         }
         st->linked = true;
@@ -504,9 +520,10 @@ int d2h_staged(Staging *st, void *dst, const void *src, size_t bytes, hipEvent_t
         LCFIR_HIP(hipEventSynchronize(st->done));
         return LCFIR_OK;
     }
+    if (tev) LCFIR_HIP(hipEventRecord(tev[3], st->stream));
     if (pinned || g_staging_mode.load(std::memory_order_relaxed) == LCFIR_STAGING_PAGEABLE) {
         LCFIR_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st->stream));
-        if (tev_end) LCFIR_HIP(hipEventRecord(tev_end, st->stream));
+        if (tev) LCFIR_HIP(hipEventRecord(tev[4], st->stream));
         LCFIR_HIP(hipStreamSynchronize(st->stream));
         return LCFIR_OK;
     }
@@ -519,7 +536,7 @@ int d2h_staged(Staging *st, void *dst, const void *src, size_t bytes, hipEvent_t
         const size_t off = i * kBounceBytes, len = std::min(kBounceBytes, bytes - off);
         LCFIR_HIP(hipMemcpyAsync(st->h_bounce[b], s + off, len, hipMemcpyDeviceToHost, st->stream));
         LCFIR_HIP(hipEventRecord(st->bev[b], st->stream));
-        if (tev_end && i + 1 == n) LCFIR_HIP(hipEventRecord(tev_end, st->stream));
+        if (tev && i + 1 == n) LCFIR_HIP(hipEventRecord(tev[4], st->stream));
         return LCFIR_OK;
     };
     for (size_t i = 0; i < n && i < 2; ++i)
@@ -663,6 +680,11 @@ int lcfir_abi_version(void) { return LCFIR_ABI_VERSION; }
 
 const char *lcfir_last_error(void) { return g_err.c_str(); }
 
+#ifndef LCFIR_BUILD_ID
+#define LCFIR_BUILD_ID "unknown"
+#endif
+const char *lcfir_build_id(void) { return LCFIR_BUILD_ID; }
+
 int lcfir_device_count(int *count) {
     if (!count) return fail(LCFIR_EINVAL, "count is null");
     int c = 0;
@@ -785,7 +807,6 @@ int lcfir_ctx_fft_units(lcfir_ctx *ctx, int32_t *outputs, int32_t *kernel, int32
     if (rc != LCFIR_OK) return rc;
     *outputs = ctx->fft.B;
     *kernel = ctx->fft.reg32 ? LCFIR_FFT_KERNEL_L32_REG
-            : ctx->fft.reg16 ? LCFIR_FFT_KERNEL_L16_REG
             : ctx->fft.L == lcfir::kFft32L ? LCFIR_FFT_KERNEL_L32_PARK : LCFIR_FFT_KERNEL_L16;
     *nrm_floats = (int32_t)lcfir::fft_nrm_unit_floats(ctx->fft);
     return LCFIR_OK;
@@ -817,9 +838,8 @@ int lcfir_ctx_set_fft_tuning(lcfir_ctx *ctx, int32_t seg_len, int32_t zero_phase
 
 int lcfir_ctx_set_fft_family(lcfir_ctx *ctx, int family) {
     if (!ctx) return fail(LCFIR_EINVAL, "ctx is null");
-    static_assert(LCFIR_FFT_FAMILY_DEFAULT == lcfir::kFamilyDefault && LCFIR_FFT_FAMILY_LDS == lcfir::kFamilyLds &&
-                  LCFIR_FFT_FAMILY_REGISTER == lcfir::kFamilyRegister);
-    if (family != LCFIR_FFT_FAMILY_DEFAULT && family != LCFIR_FFT_FAMILY_REGISTER && family != LCFIR_FFT_FAMILY_LDS)
+    static_assert(LCFIR_FFT_FAMILY_DEFAULT == lcfir::kFamilyDefault && LCFIR_FFT_FAMILY_LDS == lcfir::kFamilyLds);
+    if (family != LCFIR_FFT_FAMILY_DEFAULT && family != LCFIR_FFT_FAMILY_LDS)
         return fail(LCFIR_EINVAL, "unknown FFT kernel family %d", family);
     return retune(ctx, [&](lcfir::FftTuning &t) { t.family = family; });
 }
@@ -883,12 +903,8 @@ int lcfir_apply_range(lcfir_ctx *ctx, const float *x, int64_t n, float *y, int64
                 rc = fail(LCFIR_EDEVICE, "event creation failed");
                 break;
             }
-    if (!rc && prof && hipEventRecord(st->tev[0], st->stream) != hipSuccess)
-        rc = fail(LCFIR_EDEVICE, "event record failed");
     bool staged = false;
-    if (!rc) rc = h2d_staged(st, st->d_x, x + lo, sizeof(float) * (size_t)(hi - lo), staged);
-    if (!rc && prof && hipEventRecord(st->tev[1], st->stream) != hipSuccess)
-        rc = fail(LCFIR_EDEVICE, "event record failed");
+    if (!rc) rc = h2d_staged(st, st->d_x, x + lo, sizeof(float) * (size_t)(hi - lo), staged, prof ? st->tev : nullptr);
     if (!rc) {
         lcfir::DirectParams p{};
         p.x = st->d_x;
@@ -905,15 +921,19 @@ int lcfir_apply_range(lcfir_ctx *ctx, const float *x, int64_t n, float *y, int64
     }
     if (!rc && prof && hipEventRecord(st->tev[2], st->stream) != hipSuccess)
         rc = fail(LCFIR_EDEVICE, "event record failed");
-    if (!rc) rc = d2h_staged(st, y + start, st->d_y, sizeof(float) * (size_t)(end - start), prof ? st->tev[3] : nullptr);
+    if (!rc) rc = d2h_staged(st, y + start, st->d_y, sizeof(float) * (size_t)(end - start), prof ? st->tev : nullptr);
     if (!rc) {
         hipError_t e = hipStreamSynchronize(st->stream);
         if (e != hipSuccess) rc = fail(LCFIR_EDEVICE, "kernel failed: %s", hipGetErrorString(e));
     }
     if (!rc) {
+        // H2D = [0, 1], kernel = [1, 2] (from the samples landing), D2H = [3, 4]
         float ms[3] = {0, 0, 0};
-        if (prof)
-            for (int i = 0; i < 3; ++i) (void)hipEventElapsedTime(&ms[i], st->tev[i], st->tev[i + 1]);
+        if (prof) {
+            (void)hipEventElapsedTime(&ms[0], st->tev[0], st->tev[1]);
+            (void)hipEventElapsedTime(&ms[1], st->tev[1], st->tev[2]);
+            (void)hipEventElapsedTime(&ms[2], st->tev[3], st->tev[4]);
+        }
         const double wall =
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_call).count();
         std::lock_guard<std::mutex> lk(g_stats_mu);

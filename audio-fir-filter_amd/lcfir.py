@@ -42,8 +42,8 @@ PROGRESS_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64)
 
 STAGING_BOUNCE, STAGING_PAGEABLE = 0, 1
 # lcfir_ctx_fft_units' kernel codes (LCFIR_FFT_KERNEL_*)
-FFT_KERNELS = {0: None, 1: "l16", 2: "l32_park", 3: "l32_reg", 4: "l16_reg"}
-FFT_FAMILIES = {"default": 0, "lds": 1, "register": 2}
+FFT_KERNELS = {0: None, 1: "l16", 2: "l32_park", 3: "l32_reg"}
+FFT_FAMILIES = {"default": 0, "lds": 1}
 
 
 class RangeStats(ctypes.Structure):
@@ -63,6 +63,7 @@ _ctxp = ctypes.c_void_p
 _SIGNATURES = {
     "lcfir_abi_version": ([], _c_int),
     "lcfir_last_error": ([], ctypes.c_char_p),
+    "lcfir_build_id": ([], ctypes.c_char_p),
     "lcfir_device_count": ([ctypes.POINTER(_c_int)], _c_int),
     "lcfir_ctx_create": ([_c_int, _dp, _c_i32, ctypes.POINTER(_ctxp)], _c_int),
     "lcfir_ctx_destroy": ([_ctxp], _c_int),
@@ -168,6 +169,11 @@ def device_count() -> int:
     return c.value
 
 
+def build_id() -> str:
+    """lcfir_build_id: the loaded library's source hash (src_hash.sh)."""
+    return load().lcfir_build_id().decode()
+
+
 def _ptr(a) -> int:
     """Raw address of a numpy array or a torch tensor."""
     if isinstance(a, np.ndarray):
@@ -255,9 +261,8 @@ class Filter:
 
     def set_fft_family(self, family: str = "default"):
         """lcfir_ctx_set_fft_family for zero-phase single-partition plans:
-        "default" (fir_fft32r at L = 32 768, the LDS-column kernel at 16 384),
-        "register" (fir_fft16r at 16 384 too) or "lds" (the LDS-column
-        kernels everywhere)."""
+        "default" (fir_fft32r at L = 32 768, the LDS-column kernel at 16 384)
+        or "lds" (the LDS-column kernels everywhere)."""
         _check(load().lcfir_ctx_set_fft_family(self._ctx, FFT_FAMILIES[family]))
 
     @property

@@ -61,9 +61,9 @@ def parse():
     ap.add_argument("--ntaps", type=int, default=4001)
     ap.add_argument("--seg-len", type=int, default=0, choices=[0, 16384, 32768],
                     help="FFT segment length (0 = the library's choice)")
-    ap.add_argument("--fft-family", default="default", choices=["default", "lds", "register"],
+    ap.add_argument("--fft-family", default="default", choices=["default", "lds"],
                     help="FFT kernel family for zero-phase single-partition plans (lcfir_ctx_set_fft_family): "
-                         "register = fir_fft16r at L = 16 384 too")
+                         "lds = the LDS-column kernels at L = 32 768 too")
     ap.add_argument("--general-form", action="store_true",
                     help="FFT: the general pair table even for linear-phase taps (zero-phase form off)")
     ap.add_argument("--bits", type=int, default=24, help="0 = float32 source")
@@ -429,8 +429,29 @@ def preroll(step, seconds, sync, agree=None, batch=8):
 
 
 
-KERNEL_NAMES = {"l16": "fir_fft_f64_kernel", "l32_park": "fir_fft32_f64_kernel", "l32_reg": "fir_fft32r_kernel",
-                "l16_reg": "fir_fft16r_kernel"}
+KERNEL_NAMES = {"l16": "fir_fft_f64_kernel", "l32_park": "fir_fft32_f64_kernel", "l32_reg": "fir_fft32r_kernel"}
+
+
+def select_sidecar(paths, build_id, method, ntaps, samples_per_launch, seg_len, kernel):
+    """The first PMC sidecar (scripts/make_traffic_json.py) measured on this
+    launch shape AND on the loaded library (its build_id, lcfir_build_id()):
+    (sidecar dict, {"path", "build_id"}), or (None, None).  A sidecar without
+    a build id, or from another build, is refused -- its counters may belong
+    to a different kernel of the same name (What's weak 6)."""
+    for path in paths:
+        try:
+            with open(path) as f:
+                tj = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if not isinstance(tj, dict) or build_id in (None, "", "unknown") or tj.get("build_id") != build_id:
+            continue
+        if tj.get("method") == method and tj.get("ntaps") == ntaps and \
+                tj.get("samples_per_launch") == samples_per_launch and \
+                tj.get("seg_len", 16384 if method == "fft" else None) == seg_len and \
+                tj.get("kernel", kernel) == kernel:
+            return tj, {"path": os.path.relpath(path, ROOT), "build_id": build_id}
+    return None, None
 
 
 def fft_kernel_name(units):
@@ -625,26 +646,16 @@ def main():
             if args.normalize or peak0 > 1.0:
                 gain = 1.0 / float(np.float32(peak0))  # the pass's f64 factor (peak_scale.hpp)
             rms, npos, worst_ulp = parity_probe(x, y0, taps, sh0.start, gain)
-        traffic, f64_flops, valu_insts = None, None, None
-        # the PMC sidecar of this exact launch shape: --traffic-json, else any
-        # profiles/traffic_*.json written for it (scripts/make_traffic_json.py)
+        # the PMC sidecar of this exact launch shape AND this library build
+        # (--traffic-json, else any profiles/traffic_*.json; select_sidecar)
+        plan = flt.fft_info if method == "fft" else {}
+        kname = fft_kernel_name(flt.fft_units) if method == "fft" else "fir_direct_f64_kernel"
         sidecars = [args.traffic_json] + sorted(glob.glob(os.path.join(ROOT, "profiles", "traffic_*.json")))
-        for path in sidecars:
-            try:
-                with open(path) as f:
-                    tj = json.load(f)
-            except (OSError, ValueError):
-                continue
-            plan = flt.fft_info if method == "fft" else {}
-            kname = fft_kernel_name(flt.fft_units) if method == "fft" else "fir_direct_f64_kernel"
-            if tj.get("method") == method and tj.get("ntaps") == args.ntaps and \
-                    tj.get("samples_per_launch") == samples_per_launch and \
-                    tj.get("seg_len", 16384 if method == "fft" else None) == plan.get("seg_len") and \
-                    tj.get("kernel", kname) == kname:
-                traffic = tj.get("hbm_bytes_per_launch")
-                f64_flops = tj.get("f64_flops_per_launch")
-                valu_insts = tj.get("valu_insts_per_launch")
-                break
+        tj, traffic_source = select_sidecar(sidecars, lcfir.build_id(), method, args.ntaps, samples_per_launch,
+                                            plan.get("seg_len"), kname)
+        traffic = tj.get("hbm_bytes_per_launch") if tj else None
+        f64_flops = tj.get("f64_flops_per_launch") if tj else None
+        valu_insts = tj.get("valu_insts_per_launch") if tj else None
         # The f64 kernels are bound by VALU issue, not HBM: the launch's PMC
         # instruction counts (profiles/traffic_latest.json) over the live kernel time.
         # The resource whose floor is higher for this launch.  The direct form
@@ -708,6 +719,10 @@ def main():
                 "frac_step_note": "4 B x samples per step per GPU / ms_per_step / 8 TB/s (whole step: "
                                   "launch gaps, collective, normalize passes, lane overlap included)",
                 "traffic": traffic,
+                # where traffic / fp64_tflops_pmc / valu_issue_frac come from: the
+                # sidecar's path and the build id it was measured on (= the loaded
+                # library's), null when no sidecar matches this build and shape
+                "traffic_source": traffic_source,
                 "kernel": "fir_direct_f64_kernel" if method == "direct" else fft_kernel_name(flt.fft_units),
                 "kernel_ms": round(kern_ms, 6),
                 "kernel_ms_note": f"exclusive: {kern_launches} launches of the filter alone on one "

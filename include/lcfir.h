@@ -61,6 +61,11 @@ typedef void (*lcfir_progress_fn)(void *user, uint64_t count);
 /* ---- library --------------------------------------------------------- */
 int lcfir_abi_version(void);
 const char *lcfir_last_error(void);
+/* The library's build id: 16 hex digits of the SHA-256 of the sources it was
+ * built from (audio-fir-filter_amd/src_hash.sh), "unknown" for a build outside
+ * the Makefile.  bench.py matches PMC sidecars (profiles/traffic_*.json) to
+ * the loaded library by it. */
+const char *lcfir_build_id(void);
 int lcfir_device_count(int *count);
 
 /* ---- filter context ---------------------------------------------------- */
@@ -86,14 +91,17 @@ int lcfir_ctx_fft_info(lcfir_ctx *ctx, int32_t *seg_len, int32_t *parts, int32_t
  * overlap-save segment (B = seg_len - taps per partition + 1); *kernel: which
  * kernel runs a unit (LCFIR_FFT_KERNEL_*); *nrm_floats: the most floats of a
  * previous file's normalize (lcfir_filter_window_norm_dev) one unit carries
- * inside the filter launch, 0 when that kernel never carries one.  A call with
- * U = ceil(outputs of its first launch chunk / B) x nch units fuses the
- * normalize iff ncount <= U x *nrm_floats (and d_ny is 16-byte aligned).  All
- * 0 when the tap count is outside the FFT method's range. */
+ * inside the filter launch, 0 when that kernel never carries one.  A call
+ * fuses the normalize iff d_ny is 16-byte aligned and
+ * ceil(ceil(ncount / U) / blk) x blk <= *nrm_floats, where
+ * U = nseg x max(1, min(nch, max_units / nseg)) units share it,
+ * nseg = ceil(outputs of the call's first launch chunk / B), max_units is
+ * lcfir_ctx_set_fft_tuning's (2^31 - 1 by default) and blk = 2 048 floats on
+ * the register kernel (LCFIR_FFT_KERNEL_L32_REG), 1 024 on the others.  All 0
+ * when the tap count is outside the FFT method's range. */
 #define LCFIR_FFT_KERNEL_L16 1      /* fir_fft_f64_kernel: L = 16 384, LDS columns */
 #define LCFIR_FFT_KERNEL_L32_PARK 2 /* fir_fft32_f64_kernel: L = 32 768, two halves + park slab */
 #define LCFIR_FFT_KERNEL_L32_REG 3  /* fir_fft32r_kernel: L = 32 768 held in registers (zero-phase) */
-#define LCFIR_FFT_KERNEL_L16_REG 4  /* fir_fft16r_kernel: L = 16 384 held in registers, two workgroups per CU (zero-phase) */
 int lcfir_ctx_fft_units(lcfir_ctx *ctx, int32_t *outputs, int32_t *kernel, int32_t *nrm_floats);
 /* Diagnostic: how many previous-file normalizes (lcfir_filter_window_norm_dev
  * with ncount > 0) this ctx carried inside its filter launch (*fused) and how
@@ -102,8 +110,9 @@ int lcfir_ctx_nrm_stats(const lcfir_ctx *ctx, int64_t *fused, int64_t *separate)
 /* Explicit FFT-method choices for this ctx (the library reads no environment
  * variables).  seg_len: 0 = automatic, or 16384 / 32768.  Automatic picks the
  * length with the lower estimated time per output for the taps alone: tap
- * partitions x the measured unit cost (a 32768-sample unit costs 2.9
- * 16384-sample ones) / outputs per segment.  It never depends on a call's
+ * partitions x the measured unit cost (a 32768-sample unit costs 2.2
+ * 16384-sample ones on the register kernel, 2.9 on the park-slab kernel) /
+ * outputs per segment.  It never depends on a call's
  * shape, so every call on a ctx (range, window, channels, fft_info; every
  * thread, rank or device stage) runs the same plan and the same bytes,
  * whichever call comes first.  zero_phase: 1 = linear-phase filters run in zero-phase form (the
@@ -117,14 +126,14 @@ int lcfir_ctx_set_fft_tuning(lcfir_ctx *ctx, int32_t seg_len, int32_t zero_phase
                              int64_t max_units);
 /* Which kernel family runs the ctx's zero-phase single-partition plans:
  * DEFAULT = the transform held in registers at L = 32 768 (fir_fft32r), the
- * LDS-column kernel at L = 16 384; REGISTER = the register kernels at both
- * lengths (fir_fft16r at 16 384: two workgroups per CU); LDS = the LDS-column
- * kernels (fir_fft_f64_kernel, fir_fft32_f64_kernel), which every other plan
- * runs.  Outputs agree within 1 f32 ulp either way (tests run each); waits for
- * the ctx's queued launches and drops its plan, as lcfir_ctx_set_fft_tuning. */
+ * LDS-column kernel at L = 16 384; LDS = the LDS-column kernels
+ * (fir_fft_f64_kernel, fir_fft32_f64_kernel), which every other plan runs.
+ * Outputs agree within 1 f32 ulp either way (tests run each); waits for the
+ * ctx's queued launches and drops its plan, as lcfir_ctx_set_fft_tuning.
+ * Any other value (2 named round 5's experimental register family, now
+ * outside the library) fails with LCFIR_EINVAL. */
 #define LCFIR_FFT_FAMILY_DEFAULT 0
 #define LCFIR_FFT_FAMILY_LDS 1
-#define LCFIR_FFT_FAMILY_REGISTER 2
 int lcfir_ctx_set_fft_family(lcfir_ctx *ctx, int family);
 /* Input window [*lo, *hi) (within [0, n)) of a channel of n samples that
  * makes a call for outputs [start, end) reproduce the whole-channel call's
@@ -177,9 +186,14 @@ int lcfir_staging_set_mode(int mode);
 /* Accounting of lcfir_apply_range calls since the last reset (process-wide).
  * Always: calls, outputs, bytes each way, bounce-staged calls, the calls'
  * host wall time (summed over calls, so concurrent calls add up).  With
- * lcfir_range_profile(1) each call also records HIP events on its slot's
- * stream (a few microseconds per call): H2D span (first host chunk copy to
- * last DMA), kernel, D2H DMA span, summed over the profiled calls. */
+ * lcfir_range_profile(1) each call also records HIP events (a few
+ * microseconds per call), each on the queue that runs the step -- the
+ * device's shared link queues for page-locked buffers of >= 2 MiB, else the
+ * call's slot stream: H2D span (first DMA to last; bounce mode: first host
+ * chunk copy to last DMA), kernel (samples landed to kernel end), D2H DMA
+ * span, summed over the profiled calls.  The copy spans exclude any wait
+ * behind other calls' copies on a shared link queue (round 6; round 5's
+ * numbers included it). */
 typedef struct lcfir_range_stats {
     uint64_t calls;
     uint64_t samples;

@@ -160,10 +160,9 @@ SYM_P2 = 8 * NT
 
 
 def load_tables(prefix):
-    L_, halves, parts, tp, sym, reg32, reg16 = map(int, open(prefix + ".meta").read().split())
+    L_, halves, parts, tp, sym, reg32 = map(int, open(prefix + ".meta").read().split())
     cplx = lambda f: np.fromfile(prefix + f, np.float64).view(np.complex128)  # noqa: E731
     return {"L": L_, "halves": halves, "parts": parts, "tp": tp, "sym": bool(sym), "reg32": bool(reg32),
-            "reg16": bool(reg16),
             "pair": cplx(".pair"), "c8": cplx(".c8"), "tw": cplx(".tw"),
             "task": np.fromfile(prefix + ".task", np.uint32)}
 

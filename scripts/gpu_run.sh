@@ -11,7 +11,7 @@
 #   ab:V1,V2:REPS[:ARGS]    alternating bench lines of abvar/V1.so, abvar/V2.so, ...
 #                           (scripts/build_variant.sh builds them; "prod" = this tree's library)
 #   parity:V[:ARGS]         the FFT parity + fuzz tests with abvar/V.so in place
-#   fuzz:SEED0,CASES,NORM[,FAMILY]  seeded fuzz campaign (tests/test_gpu_fuzz.py; FAMILY: lds, register)
+#   fuzz:SEED0,CASES,NORM[,FAMILY]  seeded fuzz campaign (tests/test_gpu_fuzz.py; FAMILY: default, lds)
 #   trace[:ARGS]            tools/fft32r_trace phase timeline (default 4001 32768)
 #   vtrace:V[:ARGS]         the same tool built from variant V's source (abvar/V.trace)
 #   prof[:ARGS]             rocprofv3 --kernel-trace --stats of a bench line + the
@@ -53,6 +53,28 @@ for l in sys.stdin:
         print(d["value"], d["ms_per_step"], r["kernel_ms"], r["frac"], p.get("rms_vs_longdouble"), p.get("max_ulp"))'
 }
 LIB=audio-fir-filter_amd/liblcfir.so
+HERE_ID=$(bash audio-fir-filter_amd/src_hash.sh)
+# a variant must be built on this tree (scripts/build_variant.sh stamps
+# abvar/V.base with its base tree's build id); checked for every variant of a
+# step before anything runs
+check_variant() {
+    local v=$1 want
+    [ "$v" = prod ] && return 0
+    [ -f "abvar/$v.so" ] || { echo "!! variant $v: abvar/$v.so missing"; exit 3; }
+    want=$(sed -n 's/.*base_build_id=\([0-9a-f]*\).*/\1/p' "abvar/$v.base" 2>/dev/null)
+    if [ "$want" != "$HERE_ID" ]; then
+        echo "!! variant $v was built on tree ${want:-<unstamped>}, this tree is $HERE_ID: rebuild it (scripts/build_variant.sh)"
+        exit 3
+    fi
+}
+for S in "$@"; do # refuse stale variants before the first step runs
+    k=${S%%:*}; r=""; [ "$k" != "$S" ] && r=${S#*:}
+    case $k in
+    ab) vl=${r%%:*}; for v in ${vl//,/ }; do check_variant "$v"; done ;;
+    parity|vtrace|vdropin) check_variant "${r%%:*}" ;;
+    dropintrace) v=${r%%:*}; check_variant "${v:-prod}" ;;
+    esac
+done
 cp "$LIB" /tmp/liblcfir_prod.so
 restore() { cp /tmp/liblcfir_prod.so "$LIB"; }
 trap restore EXIT

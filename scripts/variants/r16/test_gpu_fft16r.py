@@ -7,7 +7,9 @@ Bars as tests/test_gpu_parity.py: RMS vs the long-double oracle <= 1e-9 and
 reference's thread hand-off bit-identical to the whole channel; fused peaks
 equal max |y|; within 1 ulp of the LDS-column kernel of the same segment
 length.  The index flow is modelled in scripts/fft16r_model.py (CPU test
-tests/test_fft32_tables.py runs it on the host's tables)."""
+tests/test_fft32_tables.py ran it on the host's tables while the kernel was in
+the product).  Out of the product since round 6: run it against the variant
+library (scripts/variants/r16/README.md).  "l16_reg" is kernel code 4 there."""
 import numpy as np
 import pytest
 
@@ -21,13 +23,15 @@ pytestmark = pytest.mark.gpu
 def lc():
     import lcfir
     assert lcfir.device_count() >= 1, "no GPU visible"
+    lcfir.FFT_KERNELS.setdefault(4, "l16_reg")  # the variant library's LCFIR_FFT_KERNEL_L16_REG
     return lcfir
 
 
 def r16_filter(lc, taps, **tuning):
     flt = lc.Filter(taps, method="fft")
     flt.set_fft_tuning(seg_len=16384, **tuning)
-    flt.set_fft_family("register")
+    # family 2 exists only in the variant library (scripts/variants/r16/r16_kernel.patch)
+    lc._check(lc.load().lcfir_ctx_set_fft_family(flt._ctx, 2))
     u = flt.fft_units
     assert u["kernel"] == "l16_reg" and u["outputs"] == 16384 - len(taps) + 1, u
     assert u["nrm_floats"] == 16 * 1024  # kNrmK16 blocks of 1 024 floats per unit

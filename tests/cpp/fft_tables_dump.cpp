@@ -4,8 +4,8 @@
 //
 // usage: fft_tables_dump taps.f64 seg_len zero_phase out_prefix [family]
 // (seg_len 0: the library's own choice for the taps, fft_choose_seg_len;
-// family: FftTuning::family, 0 default, 1 LDS kernels, 2 register kernels)
-// writes <out_prefix>.meta (L halves parts tp sym reg32 reg16, text), .pair .c8 .tw
+// family: FftTuning::family, 0 default, 1 LDS kernels)
+// writes <out_prefix>.meta (L halves parts tp sym reg32, text), .pair .c8 .tw
 // (complex double pairs) and .task (uint32).
 #include <cstdio>
 #include <cstdlib>
@@ -39,7 +39,7 @@ int main(int argc, char **argv) {
     const std::string out = argv[4];
     std::ofstream m(out + ".meta");
     m << T.L << " " << T.halves << " " << T.parts << " " << T.tp << " " << (T.sym ? 1 : 0) << " "
-      << (T.reg32 ? 1 : 0) << " " << (T.reg16 ? 1 : 0) << "\n";
+      << (T.reg32 ? 1 : 0) << "\n";
     dump(out + ".pair", T.pair);
     dump(out + ".task", T.task);
     dump(out + ".c8", T.c8);

@@ -1,15 +1,20 @@
 """Multi-process (gloo, CPU) tests of the batch driver's sharding and peak
-exchange.  The compute is the oracle (tests only), so these
+exchange, up to world 8 (the driver's N = 8 shapes of configs
+4 and 5).  The compute is the oracle (tests only), so these
 check the host logic: shard plans, windows, the MAX all-reduce of the
 per-file peak vector and the per-file / batch-global normalize rule, against
 a single-process run of the reference path (ProcessFile.cp:57-101)."""
 import os
 import socket
+import sys
 
 import numpy as np
 import pytest
 
 import batch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
 
 HALF = 100  # 201 taps
 
@@ -143,6 +148,14 @@ def reference(nfiles, nch, n, normalize, scope, loud):
     (2, 1, True, "file", False, True),
     (3, 2, True, "file", True, True),     # 2 files over 3 ranks (one split)
     (2, 2, True, "global", False, True),  # batch-global variant
+    # the 8-GPU shapes of configs 4 and 5 (one file per rank), rehearsed on gloo
+    (8, 8, False, "file", True, False),   # config 4: 8 files over 8 ranks, no collective
+    (8, 8, True, "file", True, True),     # config 5: --normalize, per-file peaks exchanged
+    (8, 8, True, "file", False, True),    # config 5 with every file quiet (peak < 1: forced rescale)
+    (8, 8, False, "global", True, True),  # batch-global peak (loud files rescale every file)
+    (8, 8, True, "global", False, True),
+    (8, 1, False, "file", True, True),    # one file split over 8 ranks: windows + peak exchange
+    (8, 1, True, "file", False, True),
 ])
 def test_batch_matches_serial_reference(world, nfiles, normalize, scope, loud, exchange):
     nch, n = 2, 3000
@@ -325,3 +338,54 @@ def test_bench_preroll_agrees_across_ranks():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert got[0][1] == got[1][1] and got[0][1] % 8 == 0 and got[0][1] >= 8
+
+
+def _spread_worker(rank, world, port, q):
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench  # noqa: F811 (spawned process)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        # the record bench.py's rank builds (main(): `mine`), with rank-specific values
+        mine = {"rank": rank, "device": f"0000:{0x11 + rank:02x}:00 (cuda:{rank})",
+                "ms_per_step": 1.0 + 0.01 * rank, "kernel_ms": 0.9 + 0.02 * ((rank * 5) % world),
+                "allreduce_ms_per_step": None if world == 1 else 0.1 + 0.001 * rank,
+                "samples": 345_600_000 + rank}
+        records = [None] * world
+        dist.all_gather_object(records, mine)
+        q.put((rank, bench.rank_spread(records)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rank_spread_over_8_ranks():
+    """bench.rank_spread over the 8 records an N = 8 run gathers (gloo,
+    world 8): every rank sees the same spread, in rank order, with the right
+    min / max per field -- the diagnosable N > 1 line of SCALE runs."""
+    import torch.multiprocessing as mp
+    world = 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_spread_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = sorted((q.get(timeout=120) for _ in procs), key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    spreads = [sp for _, sp in got]
+    assert all(sp == spreads[0] for sp in spreads)
+    sp = spreads[0]
+    assert sp["rank"] == list(range(world))
+    assert sp["device"] == [f"0000:{0x11 + r:02x}:00 (cuda:{r})" for r in range(world)]
+    assert sp["ms_per_step"] == [1.0 + 0.01 * r for r in range(world)]
+    assert sp["ms_per_step_min"] == 1.0 and sp["ms_per_step_max"] == 1.0 + 0.01 * 7
+    assert sp["kernel_ms_min"] == 0.9 and abs(sp["kernel_ms_max"] - (0.9 + 0.02 * 7)) < 1e-12
+    assert sp["allreduce_ms_per_step_max"] == 0.1 + 0.001 * 7
+    assert sp["samples"] == [345_600_000 + r for r in range(world)]
+    assert sp["samples_min"] == 345_600_000 and sp["samples_max"] == 345_600_007
+    # a world-1 record has no collective: the field's min / max are null
+    one = bench.rank_spread([{"rank": 0, "device": "x", "ms_per_step": 1.0, "kernel_ms": 0.9,
+                               "allreduce_ms_per_step": None, "samples": 1}])
+    assert one["allreduce_ms_per_step_min"] is None and one["allreduce_ms_per_step_max"] is None

@@ -18,7 +18,6 @@ from conftest import ROOT
 sys.path.insert(0, os.path.join(ROOT, "scripts"))
 import fft32_model as fm  # noqa: E402
 import fft32r_model as rm  # noqa: E402
-import fft16r_model as r16m  # noqa: E402
 
 DUMP = os.path.join(ROOT, "tests", "cpp", "fft_tables_dump")
 
@@ -41,20 +40,11 @@ def test_register_kernel_model_against_convolution():
     rm.main(8001)
 
 
-def test_r16_kernel_model_against_convolution():
-    """scripts/fft16r_model.py: fir_fft16r_kernel's data flow (two rounds of
-    each exchange, the 16-lane T2 groups, the special lane) with its own
-    tables, against direct convolution, at three tap counts."""
-    for ntaps in (3, 4001, 8001):
-        r16m.main(ntaps)
-
-
-# family: FftTuning::family (0 default, 1 the LDS-column kernels, 2 the register kernels)
+# family: FftTuning::family (0 default, 1 the LDS-column kernels)
 @pytest.mark.parametrize("seg_len,ntaps,sym,family", [
     (32768, 8001, True, 0), (32768, 4001, True, 0), (32768, 4003, False, 0), (32768, 8001, False, 0),
     (32768, 19201, True, 0), (16384, 4001, True, 0), (16384, 4003, False, 0), (32768, 4001, True, 1),
-    (16384, 4001, True, 2), (16384, 8001, True, 2), (16384, 4005, True, 2), (16384, 4003, False, 2),
-    (32768, 4001, True, 2)])
+    (16384, 8001, True, 1), (16384, 4005, True, 0)])
 def test_tables_emulated_segment(dump, tmp_path, seg_len, ntaps, sym, family):
     import oracle
     taps = oracle.design_lowcut(20.0, 48000.0, ntaps)
@@ -68,16 +58,11 @@ def test_tables_emulated_segment(dump, tmp_path, seg_len, ntaps, sym, family):
     # zero-phase single-partition plans: the register kernel of the segment
     # length, as the family allows
     assert tb["reg32"] == (seg_len == 32768 and sym and family != 1)
-    assert tb["reg16"] == (seg_len == 16384 and sym and family == 2)
     rng = np.random.default_rng(ntaps)
     x = rng.uniform(-1, 1, seg_len)
     if tb["reg32"]:  # the register kernel's flow on the host's task words and pair table
         c, conflicts = rm.run(taps, x, tables=tb)
         assert not conflicts
-    elif tb["reg16"]:
-        c, conflicts = r16m.run(taps, x, tables=tb)
-        # wave 0's special group: one 2-way conflict in the round-2 T2 reads
-        assert set(conflicts) <= {("T2r w0 r1", 2)}, conflicts
     else:
         c = fm.emulate(x, tb)
     half = (ntaps - 1) // 2
@@ -112,7 +97,6 @@ def test_seg_len_choice(dump, tmp_path):
         tb = fm.load_tables(str(tmp_path / "tb"))
         assert (tb["L"], tb["parts"], tb["sym"]) == (L, parts, sym and parts == 1), ntaps
         assert tb["reg32"] == (L == 32768 and parts == 1 and sym), ntaps
-        assert not tb["reg16"], ntaps  # the default family keeps the LDS kernel at 16 384
 
 
 def test_header_constants_match_model():

@@ -26,10 +26,9 @@ checks which of the two the library took (lcfir_ctx_nrm_stats).
 
 LCFIR_FUZZ_CASES / LCFIR_FUZZ_NORM_CASES / LCFIR_FUZZ_SEED0 widen or shift the
 seed range for a longer campaign (scripts/gpu_run.sh fuzz:SEED0,CASES,NORM[,FAMILY]); the defaults are the
-round-end suite's.  LCFIR_FUZZ_FAMILY (lcfir_ctx_set_fft_family: default, lds,
-register) runs the FFT cases on another kernel family: "register" puts the
-L = 16 384 zero-phase cases on fir_fft16r_kernel, "lds" the L = 32 768 ones on
-the park-slab kernel.
+round-end suite's.  LCFIR_FUZZ_FAMILY (lcfir_ctx_set_fft_family: default or
+lds) runs the FFT cases on another kernel family: "lds" puts the L = 32 768
+zero-phase cases on the park-slab kernel.
 """
 import os
 

@@ -55,3 +55,33 @@ def test_summary_and_sidecar(tmp_path):
     # the keys bench.py matches a sidecar on (bench.py, roofline.traffic)
     assert (t["method"], t["ntaps"], t["samples_per_launch"], t["seg_len"], t["kernel"]) == \
         ("fft", 4001, 57600000.0, 32768, "fir_fft32r_kernel")
+    # ... and the build it was measured on: by default the in-tree library's id
+    import lcfir
+    assert t["build_id"] == lcfir.build_id() != "unknown"
+
+
+def test_bench_refuses_a_sidecar_from_another_build(tmp_path):
+    """bench.select_sidecar attaches PMC counters only when the sidecar names
+    the loaded library's build id (lcfir_build_id) and the launch shape; the
+    line's roofline.traffic_source names the file and the id, or is null."""
+    sys.path.insert(0, ROOT)
+    import bench
+    import lcfir
+    me = lcfir.build_id()
+    base = {"method": "fft", "ntaps": 4001, "samples_per_launch": 57600000.0, "seg_len": 32768,
+            "kernel": "fir_fft32r_kernel", "hbm_bytes_per_launch": 1.0}
+    stale = tmp_path / "traffic_stale.json"      # another build of the same kernel name
+    json.dump(dict(base, build_id="0123456789abcdef", hbm_bytes_per_launch=2.0), open(stale, "w"))
+    legacy = tmp_path / "traffic_legacy.json"    # round 5's sidecars: no build id at all
+    json.dump(base, open(legacy, "w"))
+    good = tmp_path / "traffic_good.json"
+    json.dump(dict(base, build_id=me), open(good, "w"))
+    args = ("fft", 4001, 57600000.0, 32768, "fir_fft32r_kernel")
+    tj, src = bench.select_sidecar([str(stale), str(legacy)], me, *args)
+    assert tj is None and src is None
+    tj, src = bench.select_sidecar([str(stale), str(legacy), str(good)], me, *args)
+    assert tj["hbm_bytes_per_launch"] == 1.0 and src["build_id"] == me and src["path"].endswith("traffic_good.json")
+    # a matching build but another launch shape, or a library without an id
+    assert bench.select_sidecar([str(good)], me, "fft", 8001, 57600000.0, 32768, "fir_fft32r_kernel") == (None, None)
+    json.dump(dict(base, build_id="unknown"), open(good, "w"))
+    assert bench.select_sidecar([str(good)], "unknown", *args) == (None, None)
