@@ -5,8 +5,6 @@
 // phase of a steady-state unit over 64 workgroups.
 //   hipcc -O3 -std=c++2b --offload-arch=gfx950 -I../csrc fft32r_trace.hip -o fft32r_trace
 //   ./fft32r_trace [ntaps] [seg_len] [sym|asym] [nrm|-] [cus]
-// seg_len 16384 traces fir_fft16r_kernel (the register family at L = 16 384:
-// two 256-thread workgroups per CU; cus then counts CUs, the grid is 2 x cus).
 // "nrm": every launch also carries a previous file's normalize (FftNrm) of
 // n x nch floats, as config 5's fused form does.  cus: persistent-grid size
 // (default: every CU); fewer workgroups than CUs leaves the chip's memory
@@ -55,11 +53,6 @@ struct TraceProbe {
         }                                                                       \
     } while (0)
 
-static const char *kNames16[] = {"sample loads", "stage1 (dft32, tw)", "T1 w1 + BAR1", "peak + T1 r1",
-                                 "BAR2 + T1 w2 + BAR3", "T1 r2", "stage2 (2 x dft16, tw)", "pair loads + T2",
-                                 "stage3 dft16", "pair step", "inv stage3", "T2 back", "inv stage2 + T1' w1 + BAR4",
-                                 "T1' r1 + BAR5", "T1' w2 + BAR6 + r2", "final (tw, dft32)", "stores + peak"};
-constexpr int kPhases16 = 17;
 static const char *kNames[] = {"stage1 (samples, dft32, tw)", "T1 w1", "BAR1", "peak + T1 r1", "BAR2",
                                "T1 w2", "BAR3 + T1 r2", "stage2 (dft32, tw)", "pair loads A", "T2",
                                "stage3 dft16", "pair step", "inv stage3", "T2 back", "inv stage2",
@@ -104,16 +97,14 @@ int main(int argc, char **argv) {
     lcfir::FftPlan plan;
     lcfir::FftTuning tune;
     tune.seg_len = seg;
-    if (seg == 16384) tune.family = lcfir::kFamilyRegister;
     std::string err;
     if (!lcfir::fft_plan_build(plan, dt, T, tune, nullptr, err)) {
         std::fprintf(stderr, "plan: %s\n", err.c_str());
         return 1;
     }
     if (argc > 5) plan.cus = std::atoi(argv[5]);
-    const bool r16 = plan.reg16;
     {
-        const int last = r16 ? 18 : 23;
+        const int last = 23;
         CK(hipMemcpyToSymbol(HIP_SYMBOL(g_last_stamp), &last, sizeof(int)));
     }
     std::printf("plan: L %d, parts %d, zero-phase %d, B %d, grid %d\n", plan.L, plan.parts, (int)plan.sym, plan.B,
@@ -163,7 +154,7 @@ int main(int argc, char **argv) {
         }
         std::printf("fused normalize of %lld floats per launch\n", (long long)nrm.count);
     }
-    if (!plan.reg32 && !plan.reg16) {
+    if (!plan.reg32) {
         std::fprintf(stderr, "this plan runs no register kernel\n");
         return 1;
     }
@@ -172,9 +163,6 @@ int main(int argc, char **argv) {
     q.seg0 = 0;
     q.ntaps = plan.ntaps;
     auto launch = [&]() {
-        if (r16)
-            return with_nrm ? lcfir::fft16r_launch_one<lcfir::kFftOutSym, true, TraceProbe>(plan, q, nch, nullptr, err, nrm)
-                            : lcfir::fft16r_launch_one<lcfir::kFftOutSym, false, TraceProbe>(plan, q, nch, nullptr, err);
         return with_nrm ? lcfir::fft32r_launch_one<lcfir::kFftOutSym, true, TraceProbe>(plan, q, nch, nullptr, err, nrm)
                         : lcfir::fft32r_launch_one<lcfir::kFftOutSym, false, TraceProbe>(plan, q, nch, nullptr, err);
     };
@@ -204,7 +192,7 @@ int main(int argc, char **argv) {
         // workgroups resident at once per CU (from the last timed launch)
         static unsigned long long occ[kOccMax][3];
         CK(hipMemcpyFromSymbol(occ, HIP_SYMBOL(g_occ), sizeof(occ)));
-        const int nwg = (int)std::min<int64_t>((int64_t)units, (int64_t)(r16 ? 2 : 1) * plan.cus);
+        const int nwg = (int)std::min<int64_t>((int64_t)units, (int64_t)plan.cus);
         std::vector<std::pair<unsigned long long, int>> ev; // (time, +1/-1) per CU key
         std::vector<unsigned long long> keys;
         for (int b = 0; b < std::min(nwg, kOccMax); ++b) {
@@ -235,13 +223,13 @@ int main(int argc, char **argv) {
     }
     static unsigned long long tr[64][8][24];
     CK(hipMemcpyFromSymbol(tr, HIP_SYMBOL(g_fft32r_trace), sizeof(tr)));
-    const int nw = r16 ? 4 : 8, nph = r16 ? kPhases16 : kPhases;
+    const int nw = 8, nph = kPhases;
     std::printf("%-32s", "phase \\ wave");
     for (int w = 0; w < nw; ++w) std::printf("%8d", w);
     std::printf("%8s\n", "avg");
     double total[8] = {0};
     for (int ph = 0; ph < nph; ++ph) {
-        std::printf("%-32s", r16 ? kNames16[ph] : kNames[ph]);
+        std::printf("%-32s", kNames[ph]);
         double sum2 = 0;
         for (int w = 0; w < nw; ++w) {
             double acc = 0;

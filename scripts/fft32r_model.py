@@ -20,7 +20,8 @@ m = 512 a + b (thread b of 512, register a of 32), b = 16 beta + gamma.
      two tasks (column, kappa), one per round (R1, R2)
   stage 3: DFT16 over gamma -> lambda:  Z[k1 + 32 kappa + 1024 lambda]
   pair step (R1[i] with R2[15 - i]), then the same stages backwards.
-usage: fft32r_model.py [ntaps]
+usage: fft32r_model.py [ntaps]     the data-flow model
+       fft32r_model.py --price     price structural changes of the unit (price())
 """
 import sys
 
@@ -419,8 +420,83 @@ def run(taps, x_seg, tables=None):
     return c, conflicts
 
 
+# ---- pricing structural changes of the unit -----
+# Measured inputs, each from a committed file:
+#   unit and phase cycles: profiles/r06_pricing/trace_prod.log (config 2, 4 001 taps,
+#     tools/fft32r_trace.hip: per-wave s_memtime at every phase boundary, this tree)
+#   the next unit's staging DMA, priced by removing it: scripts/variants/nodma.patch
+#     (timing only, stale samples), alternating with the product on one box,
+#     profiles/r06_pricing/ab_prod_nodma.txt (launch 0.1779 -> 0.1623 ms) and its trace
+#     profiles/r06_pricing/trace_nodma.log
+#   barrier costs: the trace's BAR2 / BAR5 (barriers that follow a round, not the first
+#     of an exchange, which absorbs the older / younger waves' skew)
+#   LDS: MI355X_MICROARCH.md "LDS"; capacities from fir_fft32r.hpp (kR32Work, kR32Tw)
+PRICE = {
+    "unit_cycles": (58.9e3 + 60.3e3) / 2,   # older / younger waves' unit total (trace_prod.log)
+    "launch_ms": (0.177865 + 0.178027 + 0.178767) / 3,       # product, ab_prod_nodma.txt
+    "launch_nodma_ms": (0.162609 + 0.162073 + 0.162253) / 3,  # no staging DMA at all (timing only)
+    "round_barrier_cycles": (667 + 691) / 2,  # BAR2, BAR5 (r05 trace; r06's within 3 %)
+    "lds_round_trip_cycles": 500,           # one exposed write -> read latency of a wave-local round
+    "lds_bytes": 160 * 1024,
+    "dma_bytes": 128 * 1024,                # the next unit's samples (32 768 f32)
+    "work_array_bytes": 8 * 1088 * 16,      # kR32Work double2 (T1 / T2 / T2' / T1' and the staged samples)
+    "twiddle_bytes": (1024 + 16 + 2 + 32) * 16,  # kR32Tw + peak slots + the special lane's scratch
+}
+BUILD_BAR = 0.08
+
+
+def price(verbose=True):
+    """Price the candidate changes of fir_fft32r's unit against the product.
+    Returns {design: (feasible, net gain, best-case gain)} as fractions of the
+    launch (negative: slower); the build bar is a net gain >= BUILD_BAR.
+
+    The ceiling of every design that moves staging traffic out of the final
+    phase is measured, not modelled: the product with no staging DMA at all
+    (scripts/variants/nodma.patch, timing only) runs 8.8 % faster.  A design
+    gets at most its share of that; its extra barriers and exposed LDS
+    rounds are charged at the trace's costs."""
+    P = PRICE
+    ceiling = 1.0 - P["launch_nodma_ms"] / P["launch_ms"]
+    unit = P["unit_cycles"]
+    free_lds = P["lds_bytes"] - P["work_array_bytes"] - P["twiddle_bytes"]
+    out, lines = {}, []
+    lines.append(f"ceiling (no staging DMA at all, timing only): launch {P['launch_ms']:.4f} -> "
+                 f"{P['launch_nodma_ms']:.4f} ms = {100 * ceiling:.1f} % (build bar {100 * BUILD_BAR:.0f} %)")
+    # (B) half of the next unit's samples staged early: T2' and T1' in 4 rounds
+    # of 64 KiB so that half of every wave's region is free from T2' on; that
+    # half's DMA issued after T2', the rest in the final phase as now
+    best_b = ceiling / 2
+    cost_b = (4 * P["round_barrier_cycles"] + 4 * P["lds_round_trip_cycles"]) / unit
+    out["half_dma_early"] = (True, best_b - cost_b, best_b)
+    lines.append(f"(B) half the DMA early (T2' and T1' in 4 rounds of 64 KiB): at most {100 * best_b:.1f} %; "
+                 f"+4 barriers and +4 exposed rounds cost {100 * cost_b:.1f} %: net {100 * (best_b - cost_b):+.1f} %")
+    # (C) all of it early: the 128 KiB of samples must coexist with T1''s rounds
+    room = P["lds_bytes"] - P["dma_bytes"] - P["twiddle_bytes"]
+    rounds_c = int(np.ceil(256 * 1024 / room))
+    cost_c = (2 * (rounds_c - 2) * P["round_barrier_cycles"] + (rounds_c - 2) * P["lds_round_trip_cycles"]) / unit
+    out["all_dma_early"] = (True, ceiling - cost_c, ceiling)
+    lines.append(f"(C) all of it early: {room / 1024:.1f} KiB of LDS beside the samples -> T1' in {rounds_c} rounds "
+                 f"(+{2 * (rounds_c - 2)} barriers): at most {100 * ceiling:.1f} %, costs {100 * cost_c:.1f} %: "
+                 f"net {100 * (ceiling - cost_c):+.1f} %")
+    # (D) the final phase's twiddles W_16384^(b k1) from an LDS table: whole,
+    # 512 x 32 x 16 B; factored W_1024^(beta k1) W_16384^(gamma k1), 24 KiB,
+    # but one complex product per power (4 f64 ops) more, against the anchored
+    # chain's 3 per power it replaces
+    tab_full, tab_fact = 512 * 32 * 16, (32 * 32 + 16 * 32) * 16
+    out["final_twiddles_lds"] = (tab_fact <= free_lds, -(4 - 3) * 32 * 2 * 4.1 / unit, 0.0)
+    lines.append(f"(D) final twiddles from an LDS table: {tab_full // 1024} KiB whole / {tab_fact // 1024} KiB "
+                 f"factored against {free_lds / 1024:.1f} KiB free beside the work array and the twiddles; "
+                 f"the factored form costs 4 f64 ops per power against the chain's 3: no gain even with room")
+    if verbose:
+        print("\n".join(lines))
+    return out
+
+
 def main(ntaps=None):
     if ntaps is None:
+        if len(sys.argv) > 1 and sys.argv[1] == "--price":
+            price()
+            return
         ntaps = int(sys.argv[1]) if len(sys.argv) > 1 else 8001
     rng = np.random.default_rng(5)
     half = (ntaps - 1) // 2
