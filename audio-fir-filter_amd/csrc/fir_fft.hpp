@@ -204,13 +204,13 @@ inline int fft_partition_count(int ntaps, int L = 16384) {
 }
 // Time of one unit relative to a single-partition L = 16 384 unit, measured
 // on MI355X with tools/fft32_trace.hip (config-3 shape, 6 001 .. 30 001 taps,
-// DESIGN.md s4.2): a partitioned L = 16 384 pass also reads and writes its f64
+// CHANGELOG.md s4.2): a partitioned L = 16 384 pass also reads and writes its f64
 // partial sums; an L = 32 768 unit is two 8192-point halves plus the split,
 // the merge and the park slab, the general pair table and partitions cost
 // more there (register pressure).
 // Zero-phase single-partition L = 32768 plans run fir_fft32r_kernel (the
 // transform held in registers); its unit costs 2.2 L = 16 384 units (configs 2 and 3: 23.6 us against 10.7 us per
-// persistent-grid round), so it takes linear-phase filters
+// persistent-grid round, CHANGELOG.md s4.2), so it takes linear-phase filters
 // from ~4 000 taps (config 2's 4 001: 7.65e-5 against 8.07e-5 per output).
 constexpr double kFft32rUnitCost = 2.2;
 // FftTuning::family: the default takes fir_fft32r at L = 32 768 and the
@@ -246,7 +246,7 @@ inline double fft_seg_estimate(const std::vector<double> &h, int L, const FftTun
 // filters take L = 32 768 (one partition up to 30 721 taps instead of two
 // from 10 900, 2x faster at 12 001 .. 19 201 taps); config 1's 48 000-sample
 // launch at 19 201 taps measured equal either way (0.0386 vs 0.0387 ms, the
-// graph-replayed step 3 % faster with 32 768).
+// graph-replayed step 3 % faster with 32 768, CHANGELOG.md s0).
 inline int fft_choose_seg_len(const std::vector<double> &h, const FftTuning &tune) {
     return fft_seg_estimate(h, 32768, tune) < 0.95 * fft_seg_estimate(h, 16384, tune) ? 32768 : 16384;
 }
@@ -702,7 +702,7 @@ __device__ __forceinline__ void fft_peak_commit(const DirectParams &p, int ch, c
 // arithmetic, (float)((double)v * (1.0 / peak)), so bit-identical.  Unit u
 // takes y[u slice, (u + 1) slice); the older waves of the workgroup (0..3)
 // do it while they wait at the segment's second barrier for the younger
-// ones (DESIGN.md s8 timeline), so a batch step needs one normalize pass
+// ones (CHANGELOG.md s8 timeline), so a batch step needs one normalize pass
 // (its last file's) instead of one per file.
 struct FftNrm {
     float *y = nullptr;

@@ -52,7 +52,7 @@
 // L = 16 384 kernel's).  Now the samples are staged in LDS by LDS-DMA
 // (fft32_stage_samples) and the task words are laundered per unit: the
 // zero-phase form holds 232 VGPRs with no spills, 23 % faster.  Measured
-// against the L = 16 384 kernel (tools/fft32_trace.hip): a unit
+// against the L = 16 384 kernel (tools/fft32_trace.hip, CHANGELOG.md s4.2): a unit
 // costs 2.9x an L = 16 384 unit, so at 8 001 taps (config 3) the two are even
 // and from ~9 000 taps on, and above all where L = 16 384 needs partitions
 // (12 001 .. 30 001 taps), the longer segment wins (2x at 12 001 .. 19 201).

@@ -1,5 +1,5 @@
 // fir_fft32r.hpp -- the L = 32 768 zero-phase overlap-save unit held in
-// registers ("L = 32 768 in registers").
+// registers (its history: CHANGELOG.md s4.2).
 //
 // fir_fft32.hpp runs an L = 32 768 segment as two 8192-point halves through
 // fir_fft.hpp's column phase, parking the idle half in a global slab: 12 LDS

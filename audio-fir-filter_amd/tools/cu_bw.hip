@@ -1,6 +1,6 @@
 // cu_bw.hip -- per-CU global-memory throughput (development tool, not part of
 // the product).  The register kernels' memory phase (a unit's output stores
-// and the next unit's sample loads, DESIGN.md s4.2) and config 5's fused
+// and the next unit's sample loads, DESIGN.md s4.1) and config 5's fused
 // rescale both run at a per-CU rate well below 8 TB/s / 256; this tool
 // measures that rate by access kind: W workgroups of 1 024 threads, pinned one
 // per CU by their LDS request, streaming 16-byte accesses over a 2 GiB buffer.

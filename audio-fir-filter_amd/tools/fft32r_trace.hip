@@ -220,6 +220,32 @@ int main(int argc, char **argv) {
         }
         std::printf("residency: %d workgroups on %zu CUs; max resident per CU %d, mean of per-CU max %.2f\n",
                     (int)keys.size(), uk.size(), maxc, uk.empty() ? 0.0 : sum_max / (double)uk.size());
+        // the persistent grid's tail: each workgroup's busy span (its first
+        // unit's start to its last unit's end, 100 MHz realtime) against the
+        // launch's span; units are atomic and equal, so the launch lasts
+        // ceil(units / grid) unit times and the last round keeps only
+        // units mod grid CUs busy
+        const int nk = std::min(nwg, kOccMax);
+        unsigned long long t0 = ~0ull, t1 = 0;
+        double busy = 0;
+        std::vector<double> ends;
+        for (int b = 0; b < nk; ++b) {
+            t0 = std::min(t0, occ[b][1]);
+            t1 = std::max(t1, occ[b][2]);
+        }
+        for (int b = 0; b < nk; ++b) {
+            busy += (double)(occ[b][2] - occ[b][1]);
+            ends.push_back((double)(occ[b][2] - t0));
+        }
+        std::sort(ends.begin(), ends.end());
+        const double span = (double)(t1 - t0);
+        const int64_t full = units / nk, rem = units % nk;
+        std::printf("tail: %lld units on %d workgroups = %lld full rounds + %lld units; workgroups busy %.3f of "
+                    "the launch span (ideal %.3f = units / (grid x ceil(units / grid))); first workgroup done at "
+                    "%.3f of the span, median %.3f\n",
+                    (long long)units, nk, (long long)full, (long long)rem, busy / (nk * span),
+                    (double)units / ((double)nk * (double)(full + (rem ? 1 : 0))), ends.front() / span,
+                    ends[ends.size() / 2] / span);
     }
     static unsigned long long tr[64][8][24];
     CK(hipMemcpyFromSymbol(tr, HIP_SYMBOL(g_fft32r_trace), sizeof(tr)));

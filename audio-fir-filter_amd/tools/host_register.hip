@@ -14,7 +14,8 @@
 //   * H2D of the channel and D2H of the outputs from / to pageable memory;
 //   * the same copies once registered.
 // Registration pays off only if register + unregister (both buffers) costs less
-// than the pageable transfers minus the registered ones.
+// than the pageable transfers minus the registered ones.  Then the pageable
+// path's sensitivity to where a buffer starts (page-aligned or not).
 //   hipcc -O3 -std=c++2b --offload-arch=gfx950 host_register.hip -o host_register
 //   ./host_register [floats] [reps]
 #include <hip/hip_runtime.h>
@@ -24,6 +25,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #define CK(x)                                                                   \
@@ -105,6 +107,92 @@ int main(int argc, char **argv) {
                 bytes / med(d2h_pin) / 1e6, cost);
     std::printf("verdict: registering %s (saves %.2f ms of transfer, costs %.2f ms)\n",
                 cost < pg - pin ? "PAYS" : "does not pay", pg - pin, cost);
+
+    // Does the pageable path care where the buffer starts?  The drop-in's
+    // VectorMath storage comes from malloc (a 16-byte header in front of an
+    // mmap'd block: not page aligned), this tool's from aligned_alloc.  Same
+    // buffers every rep (warm, as a fan-out's channel is), three forms:
+    // page-aligned, +16 B, and +16 B copied as head (to the next 4 KiB
+    // boundary) + page-aligned body + tail.
+    {
+        const size_t pad = 8192;
+        char *xa = reinterpret_cast<char *>(pageable(n + pad / 4));
+        char *ya = reinterpret_cast<char *>(pageable(n + pad / 4));
+        auto copy = [&](char *hx, char *hy, bool split) {
+            double th = 0, td = 0;
+            auto t0 = clk::now();
+            if (!split) {
+                CK(hipMemcpyAsync(d, hx, bytes, hipMemcpyHostToDevice, s));
+            } else {
+                const size_t head = (4096 - (reinterpret_cast<uintptr_t>(hx) & 4095)) & 4095;
+                const size_t body = (bytes - head) / 4096 * 4096;
+                if (head) CK(hipMemcpyAsync(d, hx, head, hipMemcpyHostToDevice, s));
+                CK(hipMemcpyAsync(reinterpret_cast<char *>(d) + head, hx + head, body, hipMemcpyHostToDevice, s));
+                if (head + body < bytes)
+                    CK(hipMemcpyAsync(reinterpret_cast<char *>(d) + head + body, hx + head + body, bytes - head - body,
+                                      hipMemcpyHostToDevice, s));
+            }
+            CK(hipStreamSynchronize(s));
+            th = ms_since(t0);
+            t0 = clk::now();
+            if (!split) {
+                CK(hipMemcpyAsync(hy, d, bytes, hipMemcpyDeviceToHost, s));
+            } else {
+                const size_t head = (4096 - (reinterpret_cast<uintptr_t>(hy) & 4095)) & 4095;
+                const size_t body = (bytes - head) / 4096 * 4096;
+                if (head) CK(hipMemcpyAsync(hy, d, head, hipMemcpyDeviceToHost, s));
+                CK(hipMemcpyAsync(hy + head, reinterpret_cast<char *>(d) + head, body, hipMemcpyDeviceToHost, s));
+                if (head + body < bytes)
+                    CK(hipMemcpyAsync(hy + head + body, reinterpret_cast<char *>(d) + head + body, bytes - head - body,
+                                      hipMemcpyDeviceToHost, s));
+            }
+            CK(hipStreamSynchronize(s));
+            td = ms_since(t0);
+            return std::make_pair(th, td);
+        };
+        const char *names[3] = {"page-aligned", "+16 B", "+16 B split at 4 KiB"};
+        for (int form = 0; form < 3; ++form) {
+            std::vector<double> h, dd;
+            char *hx = form == 0 ? xa : xa + 16, *hy = form == 0 ? ya : ya + 16;
+            for (int r = 0; r < reps + 1; ++r) {
+                auto [th, td] = copy(hx, hy, form == 2);
+                if (r) { // the first is a warm-up
+                    h.push_back(th);
+                    dd.push_back(td);
+                }
+            }
+            std::printf("pageable %-22s H2D %.2f ms (%.1f GB/s)  D2H %.2f ms (%.1f GB/s)  [median of %d]\n",
+                        names[form], med(h), bytes / med(h) / 1e6, med(dd), bytes / med(dd) / 1e6, reps);
+        }
+        // the fan-out's shape: T threads, each its own stream, each moving 1/T of
+        // the +16 B buffer H2D then D2H (as T concurrent drop-in calls do)
+        for (int T : {1, 4, 16}) {
+            std::vector<hipStream_t> ss((size_t)T);
+            for (auto &q : ss) CK(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
+            std::vector<double> tot;
+            for (int r = 0; r < reps + 1; ++r) {
+                auto t0 = clk::now();
+                std::vector<std::thread> th;
+                for (int t = 0; t < T; ++t)
+                    th.emplace_back([&, t] {
+                        const size_t per = n / (size_t)T * 4, off = (size_t)t * per,
+                                     len = t == T - 1 ? bytes - off : per;
+                        CK(hipMemcpyAsync(reinterpret_cast<char *>(d) + off, xa + 16 + off, len,
+                                          hipMemcpyHostToDevice, ss[(size_t)t]));
+                        CK(hipMemcpyAsync(ya + 16 + off, reinterpret_cast<char *>(d) + off, len,
+                                          hipMemcpyDeviceToHost, ss[(size_t)t]));
+                        CK(hipStreamSynchronize(ss[(size_t)t]));
+                    });
+                for (auto &x : th) x.join();
+                if (r) tot.push_back(ms_since(t0));
+            }
+            std::printf("pageable +16 B, %2d threads x (H2D then D2H of 1/%d): %.2f ms for both directions "
+                        "(%.1f GB/s each way)\n", T, T, med(tot), bytes / med(tot) / 1e6);
+            for (auto &q : ss) CK(hipStreamDestroy(q));
+        }
+        std::free(xa);
+        std::free(ya);
+    }
     CK(hipFree(d));
     return 0;
 }

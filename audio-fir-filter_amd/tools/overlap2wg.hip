@@ -4,7 +4,7 @@
 //
 // fir_fft32r_kernel runs one 512-thread workgroup per CU; its six barriers
 // keep every wave in the same phase, so the CU's LDS pipe and its f64 VALU
-// take turns instead of overlapping (DESIGN.md s8, round 5).  This tool runs
+// take turns instead of overlapping (DESIGN.md s9).  This tool runs
 // the kernel's per-unit sequence of phases -- the same DFT32 / DFT16 /
 // twiddle-chain arithmetic (fir_fft32r.hpp) on 32 complex f64 per thread and
 // the same LDS exchanges (two workgroup rounds with barriers, two wave-local

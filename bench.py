@@ -39,7 +39,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "audio-fir-filter_amd"))
 
 HBM_PEAK_GBPS = 8000.0      # MI355X_MICROARCH.md:36 (spec)
-HBM_COPY_GBPS = 6290.0      # measured device-to-device copy rate on the box (DESIGN.md s4.3; SURVEY.md s8d)
+HBM_COPY_GBPS = 6290.0      # measured device-to-device copy rate on the box (DESIGN.md s4.5; SURVEY.md s8d)
 FP64_PEAK_TFLOPS = 78.6     # FP64 vector (spec; half the 157.3 TF FP32 vector rate)
 # f64 VALU ceiling per SIMD for the FFT kernel's own instruction mix: 1.71 ns per wave-instruction
 # (tools/valu_mix.hip, 4 waves/SIMD at the 2.4 GHz max clock; profiles/r02_valu_mix.txt)
@@ -80,7 +80,7 @@ def parse():
     ap.add_argument("--preroll-s", type=float, default=2.0,
                     help="untimed steps for this many seconds before the --warmup steps: the "
                          "shader clock ramps over the first few hundred ms of back-to-back "
-                         "launches (DESIGN.md s5), and a 20-step timed region would otherwise "
+                         "launches (CHANGELOG.md s5), and a 20-step timed region would otherwise "
                          "sit in that ramp.  0 = off")
     ap.add_argument("--kernel-launches", type=int, default=20,
                     help="launches of the filter alone, one stream, right after the pre-roll: "
@@ -533,7 +533,7 @@ def main():
     my_samples = sum(nch * (sh.end - sh.start) for sh in runner.shards)
 
     # Pre-roll: untimed steps until the shader clock has settled.  Back-to-back
-    # launches ramp it over the first few hundred ms (a 20-step
+    # launches ramp it over the first few hundred ms (CHANGELOG.md s5: a 20-step
     # region right after 5 warmup steps measured 8-20 % below steady state).
     def agree(more):
         flag = torch.tensor([1 if more else 0], dtype=torch.int32, device=dev)

@@ -1,5 +1,5 @@
 """CPU test of scripts/copy_overlap.py (the drop-in's copy-overlap analysis of
-a rocprofv3 kernel + memory-copy + HIP API trace, DESIGN.md s5): interval
+a rocprofv3 kernel + memory-copy + HIP API trace, DESIGN.md s7): interval
 unions, the H2D/D2H overlap, burst splitting and the API summary on a
 synthetic trace with known answers."""
 import csv

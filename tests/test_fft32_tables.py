@@ -77,7 +77,7 @@ def test_tables_emulated_segment(dump, tmp_path, seg_len, ntaps, sym, family):
 
 
 def test_seg_len_choice(dump, tmp_path):
-    """fft_choose_seg_len (measured unit costs): a function of
+    """fft_choose_seg_len (measured unit costs: CHANGELOG.md s4.2): a function of
     the taps alone, the per-output cost decides.  Linear-phase filters: the
     register kernel's L = 32 768 unit costs 2.2 L = 16 384 units, so 16 384 up
     to ~4 000 taps and 32 768 from config 2's 4 001 (7.65e-5 against 8.07e-5
