@@ -280,7 +280,7 @@ bool ranges_overlap(const void *a, size_t an, const void *b, size_t bn) {
 // DMA engine moves chunk i - 1 out of the other) do not beat -- 24 / 24 GB/s
 // at one thread, and 4x slower H2D per call at 16 threads (tests/cpp/
 // dropin_bench, profiles/r04_dropin/).  Caller memory that is already pinned
-// (hipHostMalloc, hipHostRegister) is copied directly in either mode.
+// by hipHostMalloc is copied directly in either mode (host_pinned).
 constexpr size_t kBounceBytes = (size_t)4 << 20;
 
 struct Staging {
@@ -369,7 +369,12 @@ lcfir_range_stats g_stats{};
 // hipHostRegister), which the DMA engine can read as a whole.  Checking only
 // the two ends would accept a range that starts in one registration, ends in
 // another and is pageable in between (hipMemcpyAsync resolves the allocation
-// from the start pointer); such a range is treated as pageable.
+// from the start pointer); such a range is treated as pageable.  ROCm 7.2's
+// hipMemGetAddressRange reports a hipHostRegister'd range's size but a null
+// base (tools/register_alias.hip, profiles/r06_dropin/register_probe.log), so
+// registered memory is not recognised here either: it goes to hipMemcpyAsync
+// as it is, and the runtime, which knows the registration, DMAs it directly
+// on the call's own stream.
 // dev (optional): the range's address in `device`'s mapping of that
 // allocation -- null if it has none, or if the allocation was made or
 // registered while another device was current (the caller then copies with

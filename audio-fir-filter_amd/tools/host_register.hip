@@ -190,6 +190,70 @@ int main(int argc, char **argv) {
                         "(%.1f GB/s each way)\n", T, T, med(tot), bytes / med(tot) / 1e6);
             for (auto &q : ss) CK(hipStreamDestroy(q));
         }
+        // the drop-in's device buffers come from the stream-ordered pool
+        // (hipMallocAsync, lcfir.hip grow()): does a pageable copy to / from
+        // pool memory take the same path as to hipMalloc'd memory?
+        {
+            void *dp = nullptr;
+            CK(hipMallocAsync(&dp, bytes, s));
+            CK(hipStreamSynchronize(s));
+            std::vector<double> h, dd;
+            for (int r = 0; r < reps + 1; ++r) {
+                auto t0 = clk::now();
+                CK(hipMemcpyAsync(dp, xa + 16, bytes, hipMemcpyHostToDevice, s));
+                CK(hipStreamSynchronize(s));
+                const double th = ms_since(t0);
+                t0 = clk::now();
+                CK(hipMemcpyAsync(ya + 16, dp, bytes, hipMemcpyDeviceToHost, s));
+                CK(hipStreamSynchronize(s));
+                if (r) {
+                    h.push_back(th);
+                    dd.push_back(ms_since(t0));
+                }
+            }
+            std::printf("pageable +16 B <-> hipMallocAsync memory: H2D %.2f ms (%.1f GB/s)  D2H %.2f ms (%.1f GB/s)\n",
+                        med(h), bytes / med(h) / 1e6, med(dd), bytes / med(dd) / 1e6);
+            CK(hipFreeAsync(dp, s));
+            CK(hipStreamSynchronize(s));
+        }
+        // per-call registration, the fan-out's shape: T threads each register
+        // a disjoint page-aligned 1/T of the channel and of the output, copy
+        // H2D and D2H from the registered slices, and unregister them
+        for (int T : {1, 4, 16}) {
+            std::vector<hipStream_t> ss((size_t)T);
+            for (auto &q : ss) CK(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
+            std::vector<double> tot, regw;
+            for (int r = 0; r < reps + 1; ++r) {
+                std::vector<double> treg((size_t)T);
+                auto t0 = clk::now();
+                std::vector<std::thread> th;
+                for (int t = 0; t < T; ++t)
+                    th.emplace_back([&, t] {
+                        const size_t per = bytes / (size_t)T / 4096 * 4096, off = (size_t)t * per,
+                                     len = t == T - 1 ? bytes - off : per;
+                        auto a = clk::now();
+                        CK(hipHostRegister(xa + off, len, hipHostRegisterDefault));
+                        CK(hipHostRegister(ya + off, len, hipHostRegisterDefault));
+                        treg[(size_t)t] = ms_since(a);
+                        CK(hipMemcpyAsync(reinterpret_cast<char *>(d) + off, xa + off, len, hipMemcpyHostToDevice,
+                                          ss[(size_t)t]));
+                        CK(hipMemcpyAsync(ya + off, reinterpret_cast<char *>(d) + off, len, hipMemcpyDeviceToHost,
+                                          ss[(size_t)t]));
+                        CK(hipStreamSynchronize(ss[(size_t)t]));
+                        CK(hipHostUnregister(xa + off));
+                        CK(hipHostUnregister(ya + off));
+                    });
+                for (auto &x : th) x.join();
+                if (r) {
+                    tot.push_back(ms_since(t0));
+                    regw.push_back(*std::max_element(treg.begin(), treg.end()));
+                }
+            }
+            std::printf("per-call registration, %2d threads x 1/%d: register (slowest thread) %.2f ms, whole "
+                        "register + H2D + D2H + unregister %.2f ms (%.1f GB/s each way)\n",
+                        T, T, med(regw), med(tot), bytes / med(tot) / 1e6);
+            for (auto &q : ss) CK(hipStreamDestroy(q));
+        }
         std::free(xa);
         std::free(ya);
     }

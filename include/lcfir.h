@@ -172,12 +172,15 @@ int lcfir_staging_count(int device, int *live, int *idle);
  * 115 MB range on MI355X).  BOUNCE: each staging slot owns two 4 MiB pinned
  * buffers; the calling thread copies chunk i into one while the DMA engine
  * moves chunk i - 1 out of the other, both ways (measured slower: 24 GB/s
- * from one thread).  Memory that is already pinned (hipHostMalloc /
- * hipHostRegister) is copied directly in both modes, on one H2D and one D2H
+ * from one thread).  Memory allocated page-locked (hipHostMalloc,
+ * lcfir_host_malloc) is copied directly in both modes, on one H2D and one D2H
  * queue per device shared by all calls (the D2H by a kernel through the
  * buffer's device mapping when both ends are 16-byte aligned), so concurrent
- * calls use the link both ways at once.  Process-wide; takes effect at the
- * next call. */
+ * calls use the link both ways at once.  hipHostRegister'd memory goes to
+ * hipMemcpyAsync as it is (the runtime DMAs it directly, on the call's own
+ * stream: ROCm 7.2 does not report a registration's extent, so the library
+ * cannot prove a range lies in one).  Process-wide; takes effect at the next
+ * call. */
 typedef enum lcfir_staging_mode {
     LCFIR_STAGING_BOUNCE = 0,
     LCFIR_STAGING_PAGEABLE = 1

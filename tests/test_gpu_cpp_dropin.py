@@ -209,9 +209,10 @@ def test_apply_range_pinned_link_queues(oracle_mod):
     through the output's device mapping when both ends are 16-byte aligned
     (else the copy engine); calls under 2 MiB keep their slot stream.  16
     threads calling at once over ranges of every alignment and tail (0..3
-    floats past a float4), into a hipHostMalloc'd and a hipHostRegister'd
-    output, equal the device call's bytes; a 7-sample call leaves its
-    neighbours untouched."""
+    floats past a float4), into a hipHostMalloc'd output (the link queues)
+    and a hipHostRegister'd one (the runtime's own path: ROCm 7.2 reports no
+    base for a registration, so host_pinned does not claim it), equal the
+    device call's bytes; a 7-sample call leaves its neighbours untouched."""
     import ctypes
     import threading
     import lcfir
