@@ -36,6 +36,16 @@ def test_abi_version():
     assert lcfir.load().lcfir_abi_version() == 1
 
 
+def test_build_id_is_the_sources_hash():
+    """lcfir_build_id() (what PMC sidecars and A/B variants are matched on)
+    is the hash audio-fir-filter_amd/src_hash.sh computes over the sources the
+    in-tree library was built from: the Makefile compiled this tree's sources,
+    not a stale one."""
+    want = subprocess.run(["bash", os.path.join(os.path.dirname(lcfir.LIB_PATH), "src_hash.sh")],
+                          capture_output=True, text=True, check=True).stdout.strip()
+    assert len(want) == 16 and lcfir.build_id() == want
+
+
 def test_even_tap_count_rejected_without_device():
     lib = lcfir.load()
     taps = np.ones(4, np.float64)
