@@ -272,15 +272,23 @@ bool ranges_overlap(const void *a, size_t an, const void *b, size_t bn) {
 }
 
 // ---- staging pool for the host-pointer entry point ------------------------
-// The reference's buffers are pageable (std::vector inside VectorMath).  By
-// default (LCFIR_STAGING_PAGEABLE) the caller's pointers go to hipMemcpyAsync
-// as they are: ROCm 7.2 moves large pageable ranges at 35 GB/s H2D and 29 GB/s
-// D2H from one thread, which a slot's own pinned bounce buffers
-// (LCFIR_STAGING_BOUNCE: the host thread copies chunk i into one while the
-// DMA engine moves chunk i - 1 out of the other) do not beat -- 24 / 24 GB/s
-// at one thread, and 4x slower H2D per call at 16 threads (tests/cpp/
-// dropin_bench, profiles/r04_dropin/).  Caller memory that is already pinned
-// by hipHostMalloc is copied directly in either mode (host_pinned).
+// The reference's buffers are pageable (std::vector inside VectorMath).
+// LCFIR_STAGING_PAGEABLE: the caller's pointers go to hipMemcpyAsync as they
+// are: ROCm 7.2 moves one thread's 115 MB range at 35-56 GB/s each way once
+// its pages are known, but pins a fresh buffer's pages on the fly and runs
+// concurrent calls' copies one at a time (a 16-thread fan-out: copy
+// concurrency 1.00, the device idle 60-70 %, profiles/r06_dropin/).
+// LCFIR_STAGING_BOUNCE: windows of kLinkMinBytes..kWinBounceMax (a fan-out's
+// share of a channel) are copied whole by the calling thread into the slot's
+// page-locked buffers, which the link queues then move both ways at once;
+// other sizes through two 4 MiB bounce chunks (slower than the runtime's path
+// for a whole channel from one thread).  LCFIR_STAGING_AUTO (the default):
+// the window bounce where it applies, the runtime's pageable path otherwise --
+// alternating on one box, the 16-thread fan-out of config 2's file moved at
+// 0.31-0.45 of the pinned-H2D bound against 0.19-0.22 pageable, 4 threads
+// 0.29-0.32 against 0.25-0.28 (profiles/r06_dropin/ab_pageable_bounce.log).
+// Caller memory that is already pinned by hipHostMalloc is copied directly in
+// every mode (host_pinned).
 constexpr size_t kBounceBytes = (size_t)4 << 20;
 
 struct Staging {
@@ -291,6 +299,10 @@ struct Staging {
     float *d_y = nullptr;
     size_t y_cap = 0;
     void *h_bounce[2] = {nullptr, nullptr}; // pinned, kBounceBytes each (lazily)
+    // BOUNCE mode, windows of kLinkMinBytes..kWinBounceMax: the whole input
+    // window and output range in page-locked buffers of the slot (grow-only)
+    void *h_win = nullptr, *h_out = nullptr;
+    size_t win_cap = 0, out_cap = 0;
     hipEvent_t bev[2] = {nullptr, nullptr}; // the last DMA touching h_bounce[b] is done
     // lcfir_range_profile: H2D start / end, kernel end, D2H start / end, each
     // recorded on the queue that runs that step (the link queues on the link
@@ -360,7 +372,12 @@ int ensure_link_events(Staging *st) {
     return LCFIR_OK;
 }
 
-std::atomic<int> g_staging_mode{LCFIR_STAGING_PAGEABLE};
+std::atomic<int> g_staging_mode{LCFIR_STAGING_AUTO};
+// the runtime's pageable path for what the mode does not bounce
+inline bool staging_runtime_path() {
+    const int m = g_staging_mode.load(std::memory_order_relaxed);
+    return m == LCFIR_STAGING_PAGEABLE || m == LCFIR_STAGING_AUTO;
+}
 std::atomic<int> g_range_profile{0};
 std::mutex g_stats_mu;
 lcfir_range_stats g_stats{};
@@ -432,6 +449,31 @@ int pcie_copy(void *dst, const void *src, size_t bytes, hipStream_t s) {
     return LCFIR_OK;
 }
 
+// BOUNCE mode for a call whose window is kLinkMinBytes..kWinBounceMax (a
+// multi-thread fan-out's share of a channel): the calling thread copies the
+// whole window into the slot's page-locked h_win and the whole output out of
+// h_out, and the DMAs between take the device's link queues as page-locked
+// caller memory does.  The runtime's pageable path instead pins the caller's
+// fresh pages on the fly and runs concurrent calls' copies one at a time
+// (profiles/r06_dropin/: copy concurrency 1.00, the device idle 60-70 % of a
+// 16-thread fan-out); the slot's buffers are pinned once and reused.  Larger
+// windows (one thread per channel) keep the chunked bounce below: one thread's
+// memcpy of a whole channel costs more than the runtime's copy.
+constexpr size_t kWinBounceMax = (size_t)32 << 20;
+int grow_host(void *&buf, size_t &cap, size_t need) {
+    if (cap >= need) return LCFIR_OK;
+    const size_t want = std::max(need, cap * 2);
+    if (buf) (void)hipHostFree(buf); // the slot's previous call has drained
+    buf = nullptr;
+    cap = 0;
+    if (hipHostMalloc(&buf, want, hipHostMallocDefault) != hipSuccess) {
+        buf = nullptr;
+        return fail(LCFIR_ENOMEM, "hipHostMalloc(%zu) for a window bounce failed", want);
+    }
+    cap = want;
+    return LCFIR_OK;
+}
+
 int ensure_bounce(Staging *st) {
     for (int b = 0; b < 2; ++b) {
         if (!st->h_bounce[b] && hipHostMalloc(&st->h_bounce[b], kBounceBytes, hipHostMallocDefault) != hipSuccess) {
@@ -474,7 +516,7 @@ int h2d_staged(Staging *st, void *dst, const void *src, size_t bytes, bool &stag
         return LCFIR_OK;
     }
     if (tev) LCFIR_HIP(hipEventRecord(tev[0], st->stream));
-    if (pinned || g_staging_mode.load(std::memory_order_relaxed) == LCFIR_STAGING_PAGEABLE) {
+    if (pinned || staging_runtime_path()) {
         LCFIR_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st->stream));
         if (tev) LCFIR_HIP(hipEventRecord(tev[1], st->stream));
         return LCFIR_OK;
@@ -526,7 +568,7 @@ int d2h_staged(Staging *st, void *dst, const void *src, size_t bytes, hipEvent_t
         return LCFIR_OK;
     }
     if (tev) LCFIR_HIP(hipEventRecord(tev[3], st->stream));
-    if (pinned || g_staging_mode.load(std::memory_order_relaxed) == LCFIR_STAGING_PAGEABLE) {
+    if (pinned || staging_runtime_path()) {
         LCFIR_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st->stream));
         if (tev) LCFIR_HIP(hipEventRecord(tev[4], st->stream));
         LCFIR_HIP(hipStreamSynchronize(st->stream));
@@ -578,6 +620,8 @@ void free_staging(Staging *s) {
         if (s->h_bounce[b]) (void)hipHostFree(s->h_bounce[b]);
         if (s->bev[b]) (void)hipEventDestroy(s->bev[b]);
     }
+    if (s->h_win) (void)hipHostFree(s->h_win);
+    if (s->h_out) (void)hipHostFree(s->h_out);
     for (hipEvent_t e : s->tev)
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : {s->ev_pre, s->ev_in, s->ev_k, s->done})
@@ -589,7 +633,11 @@ Staging *borrow_staging(int device) {
     std::unique_lock<std::mutex> lk(g_pool_mu);
     if ((int)g_pool_live.size() <= device) g_pool_live.resize((size_t)device + 1, 0);
     for (;;) {
-        for (size_t i = 0; i < g_pool.size(); ++i) {
+        // the most recently returned slot first: a fan-out of T threads keeps
+        // reusing T slots whose grow-only buffers (device, and the window
+        // bounce's page-locked ones) already fit, instead of cycling through
+        // every slot the pool has ever made
+        for (size_t i = g_pool.size(); i-- > 0;) {
             if (g_pool[i]->device == device) {
                 Staging *s = g_pool[i];
                 g_pool.erase(g_pool.begin() + (long)i);
@@ -909,7 +957,23 @@ int lcfir_apply_range(lcfir_ctx *ctx, const float *x, int64_t n, float *y, int64
                 break;
             }
     bool staged = false;
-    if (!rc) rc = h2d_staged(st, st->d_x, x + lo, sizeof(float) * (size_t)(hi - lo), staged, prof ? st->tev : nullptr);
+    const size_t xbytes = sizeof(float) * (size_t)(hi - lo), ybytes = sizeof(float) * (size_t)(end - start);
+    const int smode = g_staging_mode.load(std::memory_order_relaxed);
+    const bool bounce = smode == LCFIR_STAGING_BOUNCE || smode == LCFIR_STAGING_AUTO;
+    const bool win_x = bounce && xbytes >= kLinkMinBytes && xbytes <= kWinBounceMax && !host_pinned(x + lo, xbytes);
+    const bool win_y =
+        bounce && ybytes >= kLinkMinBytes && ybytes <= kWinBounceMax && !host_pinned(y + start, ybytes);
+    if (!rc && win_x) {
+        // the window through the slot's page-locked h_win, then the link queue
+        rc = grow_host(st->h_win, st->win_cap, xbytes);
+        if (!rc) {
+            std::memcpy(st->h_win, x + lo, xbytes);
+            rc = h2d_staged(st, st->d_x, st->h_win, xbytes, staged, prof ? st->tev : nullptr);
+            staged = true;
+        }
+    } else if (!rc) {
+        rc = h2d_staged(st, st->d_x, x + lo, xbytes, staged, prof ? st->tev : nullptr);
+    }
     if (!rc) {
         lcfir::DirectParams p{};
         p.x = st->d_x;
@@ -926,7 +990,16 @@ int lcfir_apply_range(lcfir_ctx *ctx, const float *x, int64_t n, float *y, int64
     }
     if (!rc && prof && hipEventRecord(st->tev[2], st->stream) != hipSuccess)
         rc = fail(LCFIR_EDEVICE, "event record failed");
-    if (!rc) rc = d2h_staged(st, y + start, st->d_y, sizeof(float) * (size_t)(end - start), prof ? st->tev : nullptr);
+    if (!rc && win_y) {
+        // the outputs into the slot's page-locked h_out over the link queue,
+        // then out to the caller
+        rc = grow_host(st->h_out, st->out_cap, ybytes);
+        if (!rc) rc = d2h_staged(st, st->h_out, st->d_y, ybytes, prof ? st->tev : nullptr);
+        if (!rc) std::memcpy(y + start, st->h_out, ybytes);
+        staged = true;
+    } else if (!rc) {
+        rc = d2h_staged(st, y + start, st->d_y, ybytes, prof ? st->tev : nullptr);
+    }
     if (!rc) {
         hipError_t e = hipStreamSynchronize(st->stream);
         if (e != hipSuccess) rc = fail(LCFIR_EDEVICE, "kernel failed: %s", hipGetErrorString(e));
@@ -970,7 +1043,7 @@ int lcfir_apply_range(lcfir_ctx *ctx, const float *x, int64_t n, float *y, int64
 }
 
 int lcfir_staging_set_mode(int mode) {
-    if (mode != LCFIR_STAGING_BOUNCE && mode != LCFIR_STAGING_PAGEABLE)
+    if (mode != LCFIR_STAGING_BOUNCE && mode != LCFIR_STAGING_PAGEABLE && mode != LCFIR_STAGING_AUTO)
         return fail(LCFIR_EINVAL, "unknown staging mode %d", mode);
     g_staging_mode.store(mode);
     return LCFIR_OK;

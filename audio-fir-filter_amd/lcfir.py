@@ -40,7 +40,7 @@ class LcfirError(RuntimeError):
 
 PROGRESS_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64)
 
-STAGING_BOUNCE, STAGING_PAGEABLE = 0, 1
+STAGING_BOUNCE, STAGING_PAGEABLE, STAGING_AUTO = 0, 1, 2
 # lcfir_ctx_fft_units' kernel codes (LCFIR_FFT_KERNEL_*)
 FFT_KERNELS = {0: None, 1: "l16", 2: "l32_park", 3: "l32_reg"}
 FFT_FAMILIES = {"default": 0, "lds": 1}
@@ -404,9 +404,12 @@ def staging_release(device: int = -1):
 
 
 def staging_set_mode(mode: str):
-    """lcfir_staging_set_mode: 'pageable' (default: the runtime stages the
-    caller's memory) or 'bounce' (the slot's pinned chunks)."""
-    _check(load().lcfir_staging_set_mode({"bounce": STAGING_BOUNCE, "pageable": STAGING_PAGEABLE}[mode]))
+    """lcfir_staging_set_mode: 'auto' (default: a fan-out's 2-32 MiB windows
+    through the slot's page-locked buffers, the runtime's path otherwise),
+    'pageable' (the runtime stages the caller's memory) or 'bounce' (the
+    slot's page-locked buffers for every call)."""
+    _check(load().lcfir_staging_set_mode({"bounce": STAGING_BOUNCE, "pageable": STAGING_PAGEABLE,
+                                          "auto": STAGING_AUTO}[mode]))
 
 
 def range_profile(enable: bool):

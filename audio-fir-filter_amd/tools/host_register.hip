@@ -25,6 +25,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -253,6 +254,64 @@ int main(int argc, char **argv) {
                         "register + H2D + D2H + unregister %.2f ms (%.1f GB/s each way)\n",
                         T, T, med(regw), med(tot), bytes / med(tot) / 1e6);
             for (auto &q : ss) CK(hipStreamDestroy(q));
+        }
+        // the bounce alternative, the fan-out's shape: T threads, each
+        // memcpy's its 1/T of the pageable channel into its own pinned buffer
+        // in C-byte chunks and has it DMA'd over ONE shared H2D stream, then
+        // the D2H over ONE shared D2H stream into the pinned buffer and
+        // memcpy's it out (the link both ways, the host copies in parallel)
+        for (int T : {4, 16}) {
+            const size_t per = bytes / (size_t)T;
+            std::vector<void *> pin((size_t)T);
+            for (auto &q : pin) CK(hipHostMalloc(&q, per + 4096, hipHostMallocDefault));
+            hipStream_t hin, hout;
+            CK(hipStreamCreateWithFlags(&hin, hipStreamNonBlocking));
+            CK(hipStreamCreateWithFlags(&hout, hipStreamNonBlocking));
+            std::mutex mu_in, mu_out;
+            std::vector<double> tot, mcpy;
+            for (int r = 0; r < reps + 1; ++r) {
+                std::vector<double> tm((size_t)T);
+                auto t0 = clk::now();
+                std::vector<std::thread> th;
+                for (int t = 0; t < T; ++t)
+                    th.emplace_back([&, t] {
+                        const size_t off = (size_t)t * per, len = t == T - 1 ? bytes - off : per;
+                        char *pb = static_cast<char *>(pin[(size_t)t]);
+                        hipEvent_t e;
+                        CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+                        auto a = clk::now();
+                        std::memcpy(pb, xa + 16 + off, len);
+                        double m = ms_since(a);
+                        {
+                            std::lock_guard<std::mutex> g(mu_in);
+                            CK(hipMemcpyAsync(reinterpret_cast<char *>(d) + off, pb, len, hipMemcpyHostToDevice, hin));
+                            CK(hipEventRecord(e, hin));
+                        }
+                        {
+                            std::lock_guard<std::mutex> g(mu_out);
+                            CK(hipStreamWaitEvent(hout, e, 0));
+                            CK(hipMemcpyAsync(pb, reinterpret_cast<char *>(d) + off, len, hipMemcpyDeviceToHost, hout));
+                            CK(hipEventRecord(e, hout));
+                        }
+                        CK(hipEventSynchronize(e));
+                        a = clk::now();
+                        std::memcpy(ya + 16 + off, pb, len);
+                        m += ms_since(a);
+                        tm[(size_t)t] = m;
+                        CK(hipEventDestroy(e));
+                    });
+                for (auto &x : th) x.join();
+                if (r) {
+                    tot.push_back(ms_since(t0));
+                    mcpy.push_back(*std::max_element(tm.begin(), tm.end()));
+                }
+            }
+            std::printf("bounce over shared link streams, %2d threads x 1/%d: %.2f ms for both directions "
+                        "(%.1f GB/s each way; slowest thread's two memcpys %.2f ms)\n",
+                        T, T, med(tot), bytes / med(tot) / 1e6, med(mcpy));
+            for (auto &q : pin) CK(hipHostFree(q));
+            CK(hipStreamDestroy(hin));
+            CK(hipStreamDestroy(hout));
         }
         std::free(xa);
         std::free(ya);

@@ -167,13 +167,19 @@ int lcfir_apply_range(lcfir_ctx *ctx, const float *x, int64_t n, float *y, int64
 int lcfir_staging_release(int device);
 int lcfir_staging_count(int device, int *live, int *idle);
 /* How lcfir_apply_range moves the caller's (pageable) buffers over PCIe.
- * PAGEABLE (default): the caller's pointers go to hipMemcpyAsync as they are
- * (the runtime stages them itself: 35 GB/s H2D, 29 GB/s D2H for one thread's
- * 115 MB range on MI355X).  BOUNCE: each staging slot owns two 4 MiB pinned
- * buffers; the calling thread copies chunk i into one while the DMA engine
- * moves chunk i - 1 out of the other, both ways (measured slower: 24 GB/s
- * from one thread).  Memory allocated page-locked (hipHostMalloc,
- * lcfir_host_malloc) is copied directly in both modes, on one H2D and one D2H
+ * PAGEABLE: the caller's pointers go to hipMemcpyAsync as they are (the
+ * runtime pins the pages itself: 35-56 GB/s each way for one thread's 115 MB
+ * range on MI355X, but concurrent calls' copies run one at a time).  BOUNCE:
+ * a call whose input window is 2-32 MiB (a multi-thread fan-out's share of a
+ * channel) is copied whole by the calling thread into its staging slot's
+ * page-locked buffers (grow-only, kept by the slot) and moved over the
+ * device's shared link queues, both ways at once; other calls through two
+ * 4 MiB pinned chunks (slower than the runtime for one thread's whole
+ * channel).  AUTO (the default): BOUNCE's whole-window path where it applies,
+ * PAGEABLE otherwise (config 2's 16-thread fan-out: 0.31-0.45 of the
+ * pinned-H2D bound against 0.19-0.22 pageable on one box, alternating).
+ * Memory allocated page-locked (hipHostMalloc,
+ * lcfir_host_malloc) is copied directly in every mode, on one H2D and one D2H
  * queue per device shared by all calls (the D2H by a kernel through the
  * buffer's device mapping when both ends are 16-byte aligned), so concurrent
  * calls use the link both ways at once.  hipHostRegister'd memory goes to
@@ -183,7 +189,8 @@ int lcfir_staging_count(int device, int *live, int *idle);
  * call. */
 typedef enum lcfir_staging_mode {
     LCFIR_STAGING_BOUNCE = 0,
-    LCFIR_STAGING_PAGEABLE = 1
+    LCFIR_STAGING_PAGEABLE = 1,
+    LCFIR_STAGING_AUTO = 2 /* the default */
 } lcfir_staging_mode;
 int lcfir_staging_set_mode(int mode);
 /* Accounting of lcfir_apply_range calls since the last reset (process-wide).

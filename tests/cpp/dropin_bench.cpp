@@ -13,7 +13,7 @@
 // invariance); the tool exits 3 otherwise.  This is the host-pointer rate,
 // PCIe included: never bench.py's `value`.
 //
-// usage: dropin_bench [--seconds S] [--threads a,b,...] [--reps R] [--modes pageable,bounce,pinned]
+// usage: dropin_bench [--seconds S] [--threads a,b,...] [--reps R] [--modes auto,pageable,bounce,pinned]
 //   --threads: counts; "ref" = floor(0.7 x hardware_concurrency) (main.cp:75-76)
 //   modes: the staging mode for pageable buffers, or "pinned": VectorMath's
 //   samples in page-locked memory (lcfir_host_malloc; copied directly)
@@ -90,7 +90,7 @@ static double process_file(std::vector<VectorMath<float>> &buf, const WindowedSi
 int main(int argc, char **argv) {
     double seconds = 600.0;
     int reps = 3;
-    std::string threads_arg = "1,16,ref", modes_arg = "pageable,bounce,pinned";
+    std::string threads_arg = "1,16,ref", modes_arg = "auto,pageable,bounce,pinned";
     for (int i = 1; i < argc; ++i) {
         const std::string a = argv[i];
         auto next = [&]() -> const char * {
@@ -105,7 +105,7 @@ int main(int argc, char **argv) {
         else if (a == "--reps") reps = std::max(1, std::atoi(next()));
         else if (a == "--modes") modes_arg = next();
         else {
-            std::fprintf(stderr, "usage: %s [--seconds S] [--threads a,b|ref] [--reps R] [--modes pageable,bounce,pinned]\n",
+            std::fprintf(stderr, "usage: %s [--seconds S] [--threads a,b|ref] [--reps R] [--modes auto,pageable,bounce,pinned]\n",
                          argv[0]);
             return 2;
         }
@@ -151,12 +151,14 @@ int main(int argc, char **argv) {
     const unsigned ref_threads = std::max(1u, (unsigned)(0.7 * (double)hw)); // main.cp:75-76
     int bad = 0;
     for (const std::string &mode : split(modes_arg)) {
-        if (mode != "bounce" && mode != "pageable" && mode != "pinned") {
+        if (mode != "bounce" && mode != "pageable" && mode != "pinned" && mode != "auto") {
             std::fprintf(stderr, "unknown mode %s\n", mode.c_str());
             return 2;
         }
         vectormath_pinned() = mode == "pinned";
-        if (lcfir_staging_set_mode(mode == "bounce" ? LCFIR_STAGING_BOUNCE : LCFIR_STAGING_PAGEABLE))
+        if (lcfir_staging_set_mode(mode == "bounce" ? LCFIR_STAGING_BOUNCE
+                                   : mode == "auto" ? LCFIR_STAGING_AUTO
+                                                    : LCFIR_STAGING_PAGEABLE))
             die("mode");
         for (const std::string &t : split(threads_arg)) {
             const unsigned nt = t == "ref" ? ref_threads : (unsigned)std::max(1, std::atoi(t.c_str()));

@@ -113,7 +113,7 @@ def test_dropin_bench_short(dropin):
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr + r.stdout
     lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
-    assert [(d["mode"], d["threads"]) for d in lines] == [(m, t) for m in ("pageable", "bounce", "pinned")
+    assert [(d["mode"], d["threads"]) for d in lines] == [(m, t) for m in ("auto", "pageable", "bounce", "pinned")
                                                           for t in (1, 5)]
     for d in lines:
         assert d["bit_identical"] is True and d["msamples_per_s"] > 0 and d["ntaps"] == 4001
@@ -124,7 +124,7 @@ def test_dropin_bench_short(dropin):
         assert sp["kernel"] > 0 and sp["h2d"] > 0 and sp["d2h"] > 0 and sp["wall"] > 0
 
 
-@pytest.mark.parametrize("mode,ntaps", [("bounce", 4001), ("pageable", 4001), ("pageable", 41)])
+@pytest.mark.parametrize("mode,ntaps", [("bounce", 4001), ("pageable", 4001), ("pageable", 41), ("auto", 4001)])
 def test_apply_range_staging_modes(oracle_mod, mode, ntaps):
     """lcfir_apply_range through each staging mode and from pinned host
     memory (copied directly): ranges that span several 4 MiB bounce chunks,
@@ -150,7 +150,9 @@ def test_apply_range_staging_modes(oracle_mod, mode, ntaps):
         assert np.array_equal(y, want)
         st = lcfir.range_stats(reset=True)
         assert st["calls"] == 3 and st["samples"] == n
-        assert st["staged_calls"] == (3 if mode == "bounce" else 0)
+        # bounce: every call; auto: the two 6 MB windows (the whole-window
+        # bounce), not the one-sample call (the runtime's path)
+        assert st["staged_calls"] == {"bounce": 3, "pageable": 0, "auto": 2}[mode]
         # pinned caller buffers: DMA straight from / to them
         import ctypes
         lib = lcfir.load()
@@ -196,7 +198,7 @@ def test_apply_range_staging_modes(oracle_mod, mode, ntaps):
                 for ptr in done:
                     rt.cudaHostUnregister(ptr)
     finally:
-        lcfir.staging_set_mode("pageable")  # the library's default
+        lcfir.staging_set_mode("auto")  # the library's default
     idx = np.r_[np.arange(0, 20), np.arange(n - 20, n), np.arange(1000, n, 100_003)]
     ref, _ = oracle_mod.filter_points(x, taps, idx, oracle_mod.MODE_LD)
     d = want[idx].astype(np.float64) - ref
