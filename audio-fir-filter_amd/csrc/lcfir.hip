@@ -460,18 +460,22 @@ int pcie_copy(void *dst, const void *src, size_t bytes, hipStream_t s) {
 // windows (one thread per channel) keep the chunked bounce below: one thread's
 // memcpy of a whole channel costs more than the runtime's copy.
 constexpr size_t kWinBounceMax = (size_t)32 << 20;
-int grow_host(void *&buf, size_t &cap, size_t need) {
-    if (cap >= need) return LCFIR_OK;
-    const size_t want = std::max(need, cap * 2);
+// Grow-only page-locked buffer of a slot (at most kWinBounceMax: 16 slots
+// hold at most 1 GiB, freed by lcfir_staging_release).  False when the host
+// cannot page-lock more; the caller then takes the runtime's path.
+bool grow_host(void *&buf, size_t &cap, size_t need) {
+    if (cap >= need) return true;
+    const size_t want = std::min(std::max(need, cap * 2), std::max(need, kWinBounceMax));
     if (buf) (void)hipHostFree(buf); // the slot's previous call has drained
     buf = nullptr;
     cap = 0;
     if (hipHostMalloc(&buf, want, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
         buf = nullptr;
-        return fail(LCFIR_ENOMEM, "hipHostMalloc(%zu) for a window bounce failed", want);
+        return false;
     }
     cap = want;
-    return LCFIR_OK;
+    return true;
 }
 
 int ensure_bounce(Staging *st) {
@@ -960,17 +964,16 @@ int lcfir_apply_range(lcfir_ctx *ctx, const float *x, int64_t n, float *y, int64
     const size_t xbytes = sizeof(float) * (size_t)(hi - lo), ybytes = sizeof(float) * (size_t)(end - start);
     const int smode = g_staging_mode.load(std::memory_order_relaxed);
     const bool bounce = smode == LCFIR_STAGING_BOUNCE || smode == LCFIR_STAGING_AUTO;
-    const bool win_x = bounce && xbytes >= kLinkMinBytes && xbytes <= kWinBounceMax && !host_pinned(x + lo, xbytes);
-    const bool win_y =
-        bounce && ybytes >= kLinkMinBytes && ybytes <= kWinBounceMax && !host_pinned(y + start, ybytes);
+    // (a slot that cannot page-lock its window buffers takes the runtime's path)
+    const bool win_x = bounce && xbytes >= kLinkMinBytes && xbytes <= kWinBounceMax &&
+                       !host_pinned(x + lo, xbytes) && grow_host(st->h_win, st->win_cap, xbytes);
+    const bool win_y = bounce && ybytes >= kLinkMinBytes && ybytes <= kWinBounceMax &&
+                       !host_pinned(y + start, ybytes) && grow_host(st->h_out, st->out_cap, ybytes);
     if (!rc && win_x) {
         // the window through the slot's page-locked h_win, then the link queue
-        rc = grow_host(st->h_win, st->win_cap, xbytes);
-        if (!rc) {
-            std::memcpy(st->h_win, x + lo, xbytes);
-            rc = h2d_staged(st, st->d_x, st->h_win, xbytes, staged, prof ? st->tev : nullptr);
-            staged = true;
-        }
+        std::memcpy(st->h_win, x + lo, xbytes);
+        rc = h2d_staged(st, st->d_x, st->h_win, xbytes, staged, prof ? st->tev : nullptr);
+        staged = true;
     } else if (!rc) {
         rc = h2d_staged(st, st->d_x, x + lo, xbytes, staged, prof ? st->tev : nullptr);
     }
@@ -993,8 +996,7 @@ int lcfir_apply_range(lcfir_ctx *ctx, const float *x, int64_t n, float *y, int64
     if (!rc && win_y) {
         // the outputs into the slot's page-locked h_out over the link queue,
         // then out to the caller
-        rc = grow_host(st->h_out, st->out_cap, ybytes);
-        if (!rc) rc = d2h_staged(st, st->h_out, st->d_y, ybytes, prof ? st->tev : nullptr);
+        rc = d2h_staged(st, st->h_out, st->d_y, ybytes, prof ? st->tev : nullptr);
         if (!rc) std::memcpy(y + start, st->h_out, ybytes);
         staged = true;
     } else if (!rc) {

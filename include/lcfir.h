@@ -172,7 +172,9 @@ int lcfir_staging_count(int device, int *live, int *idle);
  * range on MI355X, but concurrent calls' copies run one at a time).  BOUNCE:
  * a call whose input window is 2-32 MiB (a multi-thread fan-out's share of a
  * channel) is copied whole by the calling thread into its staging slot's
- * page-locked buffers (grow-only, kept by the slot) and moved over the
+ * page-locked buffers (grow-only, at most 32 MiB each, kept by the slot
+ * until lcfir_staging_release; a slot that cannot page-lock them takes the
+ * runtime's path) and moved over the
  * device's shared link queues, both ways at once; other calls through two
  * 4 MiB pinned chunks (slower than the runtime for one thread's whole
  * channel).  AUTO (the default): BOUNCE's whole-window path where it applies,
