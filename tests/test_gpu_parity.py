@@ -793,3 +793,32 @@ def test_padded_channel_strides(lc, oracle_mod, method, ntaps, seg_len):
             assert np.array_equal(y[:, :count], y_ref) and np.array_equal(pk, pk_ref)
     ref, _ = oracle_mod.filter_points(x[1], taps, np.arange(start, end), oracle_mod.MODE_LD)
     assert max_ulps(y_ref[1], ref) <= 1 and rms(y_ref[1], ref) <= RMS_TOL
+
+
+def test_fft_kernel_families(lc, oracle_mod):
+    """lcfir_ctx_set_fft_family: the default runs config 2's 4 001 taps on
+    the register kernel (fir_fft32r), LDS the park-slab kernel at the same
+    L = 32 768, outputs within 1 ulp of each other and of the long-double
+    oracle; round 5's experimental family 2 (fir_fft16r, now
+    scripts/variants/r16/) and unknown families fail with LCFIR_EINVAL."""
+    import synth
+    taps = oracle_mod.design_lowcut(20.0, 48000.0, 4001)
+    x = synth.file_buffer(2, 200_003, 48000.0, file=41, bits=24)
+    ys = {}
+    for fam, kernel in (("default", "l32_reg"), ("lds", "l32_park")):
+        flt = lc.Filter(taps, method="fft")
+        if fam == "lds":  # its unit costs alone would pick L = 16 384 at 4 001 taps
+            flt.set_fft_tuning(seg_len=32768)
+        flt.set_fft_family(fam)
+        assert flt.fft_info["seg_len"] == 32768 and flt.fft_units["kernel"] == kernel, fam
+        ys[fam], _ = gpu_filter_channels(lc, flt, x)
+    assert max_ulps(ys["default"], ys["lds"]) <= 1 and rms(ys["default"], ys["lds"]) <= RMS_TOL
+    idx = _sample_positions(x.shape[1], 2000, 1024, 41)
+    ref, _ = oracle_mod.filter_points(x[0], taps, idx, oracle_mod.MODE_LD)
+    assert rms(ys["default"][0][idx], ref) <= RMS_TOL and max_ulps(ys["default"][0][idx], ref) <= 1
+    flt = lc.Filter(taps, method="fft")
+    for bad in (2, 3, -1):
+        with pytest.raises(lc.LcfirError) as e:
+            lc._check(lc.load().lcfir_ctx_set_fft_family(flt._ctx, bad))
+        assert e.value.code == 1 and "family" in str(e.value)
+    assert flt.fft_units["kernel"] == "l32_reg"  # a refused family leaves the plan alone
