@@ -428,6 +428,9 @@ def run(taps, x_seg, tables=None):
 #     (timing only, stale samples), alternating with the product on one box,
 #     profiles/r06_pricing/ab_prod_nodma.txt (launch 0.1779 -> 0.1623 ms) and its trace
 #     profiles/r06_pricing/trace_nodma.log
+#   the whole memory phase, priced by removing the DMA and the output stores:
+#     scripts/variants/nodma_nostore.patch, three-way alternation on one box,
+#     profiles/r06_pricing/ab_prod_nodma_nostore.txt
 #   barrier costs: the trace's BAR2 / BAR5 (barriers that follow a round, not the first
 #     of an exchange, which absorbs the older / younger waves' skew)
 #   LDS: MI355X_MICROARCH.md "LDS"; capacities from fir_fft32r.hpp (kR32Work, kR32Tw)
@@ -435,6 +438,10 @@ PRICE = {
     "unit_cycles": (58.9e3 + 60.3e3) / 2,   # older / younger waves' unit total (trace_prod.log)
     "launch_ms": (0.177865 + 0.178027 + 0.178767) / 3,       # product, ab_prod_nodma.txt
     "launch_nodma_ms": (0.162609 + 0.162073 + 0.162253) / 3,  # no staging DMA at all (timing only)
+    # prod / no DMA / neither, alternating (ab_prod_nodma_nostore.txt)
+    "ab3_launch_ms": (0.18036 + 0.179066 + 0.17924) / 3,
+    "ab3_nodma_ms": (0.162822 + 0.162772 + 0.1631) / 3,
+    "ab3_nomem_ms": (0.160374 + 0.160546 + 0.160434) / 3,
     "round_barrier_cycles": (667 + 691) / 2,  # BAR2, BAR5 (r05 trace; r06's within 3 %)
     "lds_round_trip_cycles": 500,           # one exposed write -> read latency of a wave-local round
     "lds_bytes": 160 * 1024,
@@ -443,6 +450,13 @@ PRICE = {
     "twiddle_bytes": (1024 + 16 + 2 + 32) * 16,  # kR32Tw + peak slots + the special lane's scratch
 }
 BUILD_BAR = 0.08
+
+
+def memory_phase_ceiling():
+    """(no-DMA gain, no-DMA-and-no-stores gain) of the three-way alternation:
+    what any change to the unit's HBM traffic can take at most."""
+    P = PRICE
+    return 1.0 - P["ab3_nodma_ms"] / P["ab3_launch_ms"], 1.0 - P["ab3_nomem_ms"] / P["ab3_launch_ms"]
 
 
 def price(verbose=True):
@@ -487,6 +501,10 @@ def price(verbose=True):
     lines.append(f"(D) final twiddles from an LDS table: {tab_full // 1024} KiB whole / {tab_fact // 1024} KiB "
                  f"factored against {free_lds / 1024:.1f} KiB free beside the work array and the twiddles; "
                  f"the factored form costs 4 f64 ops per power against the chain's 3: no gain even with room")
+    dma3, mem3 = memory_phase_ceiling()
+    lines.append(f"ceiling of the whole memory phase (no DMA and no output stores, timing only): "
+                 f"{100 * mem3:.1f} % (no DMA alone {100 * dma3:.1f} % in the same alternation): "
+                 f"no memory-side change of the unit can take more")
     if verbose:
         print("\n".join(lines))
     return out

@@ -121,3 +121,7 @@ def test_structural_changes_priced_below_the_bar():
         assert net < rm.BUILD_BAR, name
     assert out["half_dma_early"][2] < rm.BUILD_BAR  # even for free
     assert not out["final_twiddles_lds"][0]
+    # no DMA and no stores at all (the unit touches no HBM after its samples):
+    # the stores add only 1-2 % once the DMA is gone, whole phase < 12 %
+    dma3, mem3 = rm.memory_phase_ceiling()
+    assert 0.08 < dma3 < mem3 < 0.12 and mem3 - dma3 < 0.03
