@@ -5,26 +5,18 @@ check the host logic: shard plans, windows, the MAX all-reduce of the
 per-file peak vector and the per-file / batch-global normalize rule, against
 a single-process run of the reference path (ProcessFile.cp:57-101)."""
 import os
-import socket
 import sys
 
 import numpy as np
 import pytest
 
 import batch
+import gloo_ranks
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 
 HALF = 100  # 201 taps
-
-
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
 
 
 def make_files(nfiles, nch, n, loud):
@@ -77,46 +69,30 @@ class OracleBackend(batch.Backend):
             yw[:] = (yw.astype(np.float64) * (1.0 / p)).astype(np.float32)
 
 
-def _worker(rank, world, port, nfiles, nch, n, normalize, scope, loud, q):
+def _worker(rank, world, nfiles, nch, n, normalize, scope, loud):
     import torch
     import torch.distributed as dist
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
-                            world_size=world)
-    try:
-        files = make_files(nfiles, nch, n, loud)
-        taps = make_taps()
+    files = make_files(nfiles, nch, n, loud)
+    taps = make_taps()
 
-        def allreduce(peaks):
-            t = torch.from_numpy(peaks)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    def allreduce(peaks):
+        t = torch.from_numpy(peaks)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
 
-        r = batch.BatchRunner(OracleBackend(taps), rank, world, [f.shape[1] for f in files], nch,
-                              HALF, normalize, scope, allreduce)
-        r.prepare(lambda f, lo, hi: files[f][:, lo:hi])
-        # three steps: with an exchange each step's normalize rides in the next
-        # step's filter launches (BatchRunner defer); results() runs the last
-        # step's pending ones
-        for _ in range(3):
-            r.step()
-        q.put((rank, r.exchange, [(sh, y.copy()) for sh, y in r.results()], r.peaks.copy()))
-    finally:
-        dist.destroy_process_group()
+    r = batch.BatchRunner(OracleBackend(taps), rank, world, [f.shape[1] for f in files], nch,
+                          HALF, normalize, scope, allreduce)
+    r.prepare(lambda f, lo, hi: files[f][:, lo:hi])
+    # three steps: with an exchange each step's normalize rides in the next
+    # step's filter launches (BatchRunner defer); results() runs the last
+    # step's pending ones
+    for _ in range(3):
+        r.step()
+    return rank, r.exchange, [(sh, y.copy()) for sh, y in r.results()], r.peaks.copy()
 
 
 def run_dist(world, nfiles, nch, n, normalize, scope, loud):
-    import torch.multiprocessing as mp
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, nfiles, nch, n, normalize, scope,
-                                                loud, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    got = [q.get(timeout=120) for _ in procs]
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    return got
+    """The ranks' (rank, exchange, results, peaks), one gloo group (tests/gloo_ranks.py)."""
+    return gloo_ranks.run(_worker, world, (nfiles, nch, n, normalize, scope, loud))
 
 
 def reference(nfiles, nch, n, normalize, scope, loud):
@@ -292,15 +268,13 @@ def test_force_exchange_defers_normalize(lanes, normalize, scope, nfiles):
     r.close()
 
 
-def _preroll_worker(rank, world, port, q):
+def _preroll_worker(rank, world):
     import time
     import torch
     import sys
     import torch.distributed as dist
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
-                            world_size=world)
 
     def step():  # a step with a peak exchange: a collective, slower on rank 1
         t = torch.zeros(1)
@@ -317,8 +291,7 @@ def _preroll_worker(rank, world, port, q):
     # rank 0 would go on stepping into a collective rank 1 never joins
     n = bench.preroll(step, 0.25 if rank == 0 else 0.1, lambda: None, agree)
     dist.barrier()
-    q.put((rank, n, time.perf_counter() - t0))
-    dist.destroy_process_group()
+    return rank, n, time.perf_counter() - t0
 
 
 def test_bench_preroll_agrees_across_ranks():
@@ -326,54 +299,30 @@ def test_bench_preroll_agrees_across_ranks():
     collective, so the ranks must run the same number of steps.  preroll()
     lets them agree after every batch (gloo, world 2, different budgets and
     step times): same count on both ranks, no deadlock."""
-    import torch.multiprocessing as mp
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_preroll_worker, args=(r, 2, port, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    got = sorted(q.get(timeout=120) for _ in procs)
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+    got = gloo_ranks.run(_preroll_worker, 2)
     assert got[0][1] == got[1][1] and got[0][1] % 8 == 0 and got[0][1] >= 8
 
 
-def _spread_worker(rank, world, port, q):
+def _spread_worker(rank, world):
     import torch.distributed as dist
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench  # noqa: F811 (spawned process)
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
-    try:
-        # the record bench.py's rank builds (main(): `mine`), with rank-specific values
-        mine = {"rank": rank, "device": f"0000:{0x11 + rank:02x}:00 (cuda:{rank})",
-                "ms_per_step": 1.0 + 0.01 * rank, "kernel_ms": 0.9 + 0.02 * ((rank * 5) % world),
-                "allreduce_ms_per_step": None if world == 1 else 0.1 + 0.001 * rank,
-                "samples": 345_600_000 + rank}
-        records = [None] * world
-        dist.all_gather_object(records, mine)
-        q.put((rank, bench.rank_spread(records)))
-    finally:
-        dist.destroy_process_group()
+    # the record bench.py's rank builds (main(): `mine`), with rank-specific values
+    mine = {"rank": rank, "device": f"0000:{0x11 + rank:02x}:00 (cuda:{rank})",
+            "ms_per_step": 1.0 + 0.01 * rank, "kernel_ms": 0.9 + 0.02 * ((rank * 5) % world),
+            "allreduce_ms_per_step": None if world == 1 else 0.1 + 0.001 * rank,
+            "samples": 345_600_000 + rank}
+    records = [None] * world
+    dist.all_gather_object(records, mine)
+    return rank, bench.rank_spread(records)
 
 
 def test_rank_spread_over_8_ranks():
     """bench.rank_spread over the 8 records an N = 8 run gathers (gloo,
     world 8): every rank sees the same spread, in rank order, with the right
     min / max per field -- the diagnosable N > 1 line of SCALE runs."""
-    import torch.multiprocessing as mp
     world = 8
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_spread_worker, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    got = sorted((q.get(timeout=120) for _ in procs), key=lambda t: t[0])
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+    got = gloo_ranks.run(_spread_worker, world)
     spreads = [sp for _, sp in got]
     assert all(sp == spreads[0] for sp in spreads)
     sp = spreads[0]

@@ -114,36 +114,20 @@ def test_rank_spread_reduction():
     assert r["allreduce_ms_per_step"] == [None, None] and r["allreduce_ms_per_step_max"] is None
 
 
-def _gather_worker(rank, world, port, q):
+def _gather_worker(rank, world):
     import torch.distributed as dist
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     mine = {"rank": rank, "device": f"cpu{rank}", "ms_per_step": 1.0 + rank, "kernel_ms": 0.5,
             "allreduce_ms_per_step": 0.1 * (rank + 1), "samples": 100 * (rank + 1)}
     records = [None] * world
     dist.all_gather_object(records, mine)
-    if rank == 0:
-        q.put(bench.rank_spread(records))
-    dist.barrier()
-    dist.destroy_process_group()
+    return bench.rank_spread(records) if rank == 0 else None
 
 
 @pytest.mark.timeout(120)
 def test_rank_spread_gathered_over_gloo():
     """bench.py's all_gather_object of the per-rank records, world 2 on gloo."""
-    import socket
-    import torch.multiprocessing as mp
-    with socket.socket() as so:
-        so.bind(("127.0.0.1", 0))
-        port = so.getsockname()[1]
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    procs = [ctx.Process(target=_gather_worker, args=(r, 2, port, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    r = q.get(timeout=100)
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+    import gloo_ranks
+    r = gloo_ranks.run(_gather_worker, 2, timeout=100)[0]
     assert r["rank"] == [0, 1] and r["device"] == ["cpu0", "cpu1"]
     assert r["ms_per_step_max"] == 2.0 and r["samples"] == [100, 200]
     assert r["allreduce_ms_per_step_max"] == pytest.approx(0.2)
